@@ -1,0 +1,247 @@
+"""Headline benchmark: pCN steps/s on Lorenz-96 d=40, 2000 RK4 steps, 65 536 chains.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N > 1: launched by torch.distributed.run, one process per GPU)
+
+A "step" is one pCN sweep: every chain of the batch proposes, runs its
+forward map (2000 RK4 steps of Lorenz-96, d=40), evaluates Φ and accepts or
+rejects -- one launch of the fused libipmc kernel.  Each GPU owns 65 536
+chains (weak scaling; global chain ids rank*65536 + i), inputs resident in
+HBM before the timed region.  value = all chains of all ranks x K / max-rank
+wall time.  Arithmetic: float64 (the reference computes in float64); the
+float32 throughput of the same workload is reported in "extra".
+
+roofline: VALU-bound (no MFMA, no HBM traffic inside the RK loop). achieved =
+algorithmic FLOP per launch / average kernel time from HIP events on the
+launch stream; algorithmic FLOP per pCN step per chain = 30·d·n = 2.4 MFLOP
+(SURVEY §8(d) counting rule).
+cpu_baseline: the C oracle (same arithmetic, bit-exact), a bounded sample of
+the same workload on this host's cores, rank 0 at N=1 only.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from ip_mcmc_amd import Lorenz96Operator, _abi  # noqa: E402
+from ip_mcmc_amd._lib import call  # noqa: E402
+
+D, N_RK, DT, BETA, GAMMA = 40, 2000, 0.005, 0.2, 0.1
+CHAINS_PER_GPU = 65536
+FLOP_PER_STEP = 30 * D * N_RK  # 2.4e6
+PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}  # MI355X vector (spec), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def problem():
+    """Config 3: forcing-field inverse problem."""
+    op = Lorenz96Operator(D, forcing_mean=8.0, dt=DT, n_steps=N_RK)  # x0: 1000-step spin-up from 8 + 0.01 e0
+    k = np.arange(D)
+    u_true = 0.5 * np.sin(2 * np.pi * k / D)  # F_true = 8 + 0.5 sin(2πk/40)
+    g_true = op(u_true)
+    y = g_true + GAMMA * np.random.default_rng(3).normal(size=D)
+    return op, y
+
+
+class Workload:
+    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0):
+        self.dev, self.dtype = dev, dtype
+        self.model, self._keep = op.model(dtype, dev)
+        t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
+        self.y, self.ginv, self.sq = t(y), t(np.full(D, 1 / GAMMA)), t(np.ones(D))
+        self.u = torch.zeros((n_chains, D), dtype=dtype, device=dev)
+        self.phi = torch.empty(n_chains, dtype=dtype, device=dev)
+        self.acc = torch.zeros(n_chains, dtype=torch.int64, device=dev)
+        self.stream = torch.cuda.current_stream(dev).cuda_stream
+        adt = _abi.F64 if dtype == torch.float64 else _abi.F32
+        call("ipmc_potential", C.byref(self.model), adt, n_chains, self.u.data_ptr(), self.y.data_ptr(),
+             self.ginv.data_ptr(), self.phi.data_ptr(), self.stream)
+        s = _abi.IpmcSweep()
+        s.dtype, s.lanes_per_chain = adt, lanes
+        s.n_chains, s.chain_offset = n_chains, chain_offset
+        s.u, s.phi, s.accepts = self.u.data_ptr(), self.phi.data_ptr(), self.acc.data_ptr()
+        s.y, s.gamma_inv, s.prior_sqrt = self.y.data_ptr(), self.ginv.data_ptr(), self.sq.data_ptr()
+        s.beta, s.contraction = BETA, float(np.sqrt(1 - BETA**2))
+        s.seed, s.step0, s.n_steps = 2, 0, 1
+        self.s = s
+        self.lanes = call_auto(self.model, adt, n_chains) if lanes == 0 else lanes
+
+    def step(self):
+        call("ipmc_pcn_sweep", C.byref(self.model), C.byref(self.s), self.stream)
+        self.s.step0 += 1
+
+
+def call_auto(model, adt, n):
+    from ip_mcmc_amd._lib import lib
+
+    return lib().ipmc_auto_lanes(C.byref(model), adt, n)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def timed(w, steps, warmup, world):
+    for _ in range(warmup):
+        w.step()
+    torch.cuda.synchronize(w.dev)
+    barrier(world)
+    torch.cuda.synchronize(w.dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record()
+        w.step()
+        b.record()
+    torch.cuda.synchronize(w.dev)
+    barrier(world)
+    torch.cuda.synchronize(w.dev)
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=w.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, kern_ms
+
+
+def cpu_baseline(op, y, dtype_np, budget_s=15.0):
+    """The C oracle on this host's cores: a bounded sample of the same
+    workload (chains x 1 pCN step), scaled to pCN steps/s."""
+    sys.path.insert(0, REPO)
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+
+    def run(nc):
+        U = np.zeros((nc, D), dtype=dtype_np)
+        ginv = np.full(D, 1 / GAMMA)
+        phi = O.potential(op, U, y, ginv, dtype_np)
+        acc = np.zeros(nc, dtype=np.int64)
+        t0 = time.perf_counter()
+        O.pcn_sweep(op, U, phi, y, ginv, np.ones(D), BETA, 2, 0, 1, accepts=acc, n_threads=threads)
+        return time.perf_counter() - t0
+
+    t1 = run(threads)  # one chain-step per thread, calibration
+    per = t1 / threads
+    n = int(max(threads, min(1_000_000, budget_s / max(per, 1e-6) * threads * 0.8)))
+    n = (n // threads) * threads
+    el = run(n)
+    return {"value": n / el, "unit": "pCN steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} chains x 1 pCN step of the headline workload (d=40, 2000 RK4 steps, "
+                      f"{'f64' if dtype_np == np.float64 else 'f32'}), C oracle, {threads} threads, {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--chains", type=int, default=CHAINS_PER_GPU, help="chains per GPU")
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    op, y = problem()
+    tdt = torch.float64 if args.dtype == "f64" else torch.float32
+    w = Workload(op, y, args.chains, rank * args.chains, tdt, dev, args.lanes)
+    el, kern_ms = timed(w, args.steps, args.warmup, world)
+    total_steps = world * args.chains * args.steps
+    value = total_steps / el
+
+    # final gather of the per-chain results (the path's one exchange): accept
+    # rate and posterior-mean state over all chains of all ranks
+    from ip_mcmc_amd.shard import gather_chains
+
+    acc_all = gather_chains(w.acc.view(-1, 1), world * args.chains)
+    accept_rate = float(acc_all.double().sum().item()) / (world * args.chains * (args.steps + args.warmup))
+
+    extra = {}
+    if not args.no_extra:
+        other = torch.float32 if tdt == torch.float64 else torch.float64
+        w2 = Workload(op, y, args.chains, rank * args.chains, other, dev, args.lanes)
+        el2, k2 = timed(w2, args.steps, args.warmup, world)
+        key = "f32" if other == torch.float32 else "f64"
+        extra[f"{key}_pcn_steps_per_s"] = world * args.chains * args.steps / el2
+        extra[f"{key}_kernel_ms"] = k2
+        extra[f"{key}_tflops"] = args.chains * FLOP_PER_STEP / (k2 * 1e-3) / 1e12
+        del w2
+
+    flop = args.chains * FLOP_PER_STEP
+    achieved = flop / (kern_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    hbm_bytes = args.chains * D * (2 if tdt == torch.float32 else 4) * 2 * 2  # u read+write, sq/y/.. via cache
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(op, y, np.float64 if tdt == torch.float64 else np.float32)
+
+    if rank == 0:
+        line = {
+            "metric": "pCN steps/sec (whole node), Lorenz-96 d=40 T=2000, 65 536 chains",
+            "value": value,
+            "unit": "pCN steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (forcing-field inverse problem, y = G(u_true) + N(0, 0.1^2), seed 3)",
+            "config": {
+                "workload": "lorenz96_d40_rk4_2000_pcn",
+                "chains_per_gpu": args.chains,
+                "total_chains": world * args.chains,
+                "d": D,
+                "rk4_steps": N_RK,
+                "dt": DT,
+                "beta": BETA,
+                "arith": "fma",
+                "lanes_per_chain": w.lanes,
+                "parallelism": f"chains sharded over {world} GPU(s)",
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": peak,
+                "unit": "TFLOP/s",
+                "frac": achieved / peak,
+                "traffic": None,
+                "kernel_ms": kern_ms,
+                "flop_per_launch": flop,
+                "note": "vector-ALU bound; algorithmic FLOP = 30*d*n per chain-step; "
+                        f"HBM ~{hbm_bytes / (kern_ms * 1e-3) / 1e9:.2f} GB/s of {HBM_PEAK_GBS:.0f}",
+            },
+            "cpu_baseline": cpu,
+            "accept_rate": accept_rate,
+            "extra": extra,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+/*
+ * ipmc.h — C-ABI of the MI355X many-chain pCN sampler (libipmc.so).
+ *
+ * This is the drop-in boundary for the reference's hot path, the pCN
+ * Metropolis–Hastings step with an evolution-equation misfit potential:
+ *
+ *   reference (ochsnerd/ip_mcmc, pure Python, one chain)      this ABI (many chains, device)
+ *   ------------------------------------------------------    -----------------------------------
+ *   MCMCSampler.run / _step           sampler.py:12-41        ipmc_pcn_sweep   (n_steps steps/launch)
+ *   ConstSteppCNProposer.__call__     proposer.py:81-82       ipmc_pcn_sweep   (proposal stage)
+ *   VarSteppCNProposer.__call__       proposer.py:110-115     ipmc_pcn_sweep   (host passes beta per launch)
+ *   ProbabilisticAccepter.__call__    accepter.py:59-62       ipmc_pcn_sweep   (accept stage)
+ *   pCNAccepter.accept_probability    accepter.py:121-122     ipmc_pcn_sweep   (exp(Φu−Φv) > r)
+ *   CountedAccepter.__call__          accepter.py:20-27       ipmc_sweep.accepts (per-chain counter)
+ *   ConstrainAccepter.__call__        accepter.py:52-55       ipmc_sweep.box_lo/box_hi/box_off
+ *   EvolutionPotential.__call__       potential.py:53-54      ipmc_potential
+ *   G(u) observation operators        lorenz_mcmc.py:55-68,   ipmc_forward
+ *                                     stuart_examples.py:69-70,
+ *                                     burgers/utilities.py:40-41
+ *   GaussianDistribution.sample       distribution.py:114-118 ipmc_normal (counter-based N(0,I))
+ *
+ * The reference has no FFI of its own (it is duck-typed Python); these entry
+ * points are what a ctypes binding of its plugin API binds.
+ *
+ * Conventions
+ *  - Every pointer inside the structs and every data pointer argument is a
+ *    DEVICE pointer (hipMalloc / torch CUDA tensor) for libipmc.so; the CPU
+ *    oracle (oracle/liboracle.so) implements the same structs on HOST pointers.
+ *  - Arrays are dense row-major; per-chain arrays are [n_chains, k] with k
+ *    contiguous. Real arrays have the dtype given by `dtype` (float or double).
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *    Calls are asynchronous on that stream and never synchronise the host.
+ *  - Return value: IPMC_OK or an ipmc_status error; ipmc_last_error() gives
+ *    a message (thread-local).
+ *  - Randomness is counter-based (Philox4x32-10). The draw for (chain, step,
+ *    component) is a pure function of (seed, global chain id, global pCN step,
+ *    component), so results do not depend on sharding or launch splitting.
+ */
+#ifndef IPMC_H
+#define IPMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPMC_ABI_VERSION 1
+
+typedef enum {
+  IPMC_OK = 0,
+  IPMC_ERR_INVALID = 1,     /* bad argument (shape, null pointer, range) */
+  IPMC_ERR_UNSUPPORTED = 2, /* valid request the library does not implement */
+  IPMC_ERR_DEVICE = 3       /* HIP runtime error (launch / memory) */
+} ipmc_status;
+
+typedef enum { IPMC_F32 = 0, IPMC_F64 = 1 } ipmc_dtype;
+
+typedef enum {
+  IPMC_MODEL_LINEAR = 0,    /* G(u) = A (theta0 + u)                  stuart_examples.py:69-70 */
+  IPMC_MODEL_LORENZ63 = 1,  /* RK4 Lorenz-63, moments time-averaged   (no reference; lorenz_mcmc.py:17-40 pattern) */
+  IPMC_MODEL_LORENZ96 = 2,  /* RK4 single-scale Lorenz-96, forcing field theta0+u, time-averaged X   lorenz.py:73-88 */
+  IPMC_MODEL_BURGERS = 3    /* Rusanov FV + SSPRK2 Burgers, windowed trapz observations   burgers/rusanov.py, utilities.py */
+} ipmc_model_kind;
+
+typedef enum {
+  IPMC_ARITH_FMA = 0,       /* fused multiply-add form (fast path, bit-exact vs oracle in the same mode) */
+  IPMC_ARITH_REFERENCE = 1  /* no FMA anywhere; reference expression order (lorenz.py:77-81) */
+} ipmc_arith;
+
+typedef enum { IPMC_DT_FIXED = 0, IPMC_DT_CFL = 1 } ipmc_dt_mode;
+
+/* Forward-map description. Fields not used by a model are ignored. */
+typedef struct ipmc_model {
+  int32_t kind;       /* ipmc_model_kind */
+  int32_t arith;      /* ipmc_arith */
+  int32_t k;          /* parameter dimension (length of u) */
+  int32_t q;          /* observation dimension (length of G(u)) */
+  int32_t dim;        /* state dimension: L96 d; Burgers N interior cells; L63 3 */
+  int32_t n_steps;    /* time steps of the integrator (fixed-dt models) */
+  double dt;          /* time step */
+  const void* x0;     /* [dim] initial state (L63/L96); Burgers: [dim+2] cell centres incl. ghosts */
+  const void* theta0; /* [k] prior-mean offset: the model evaluates at theta = theta0 + u */
+  const void* A;      /* LINEAR: [q, k] matrix */
+  /* Burgers (IPMC_MODEL_BURGERS) */
+  int32_t dt_mode;    /* ipmc_dt_mode */
+  int32_t n_windows;  /* == q */
+  const int32_t* win_lo; /* [q] first cell (interior index) of each trapz window  utilities.py:93-98 */
+  const int32_t* win_hi; /* [q] one-past-last cell */
+  double dx;          /* cell width (reference: linspace retstep) */
+  double t_end;       /* CFL mode: integrate while t < t_end (rusanov.py:40-45) */
+  double cfl;         /* CFL mode: dt = cfl*dx/max|u| (reference 0.5, rusanov.py:102-109) */
+  double nu;          /* viscosity of the optional central-difference term (0 = reference scheme) */
+  double meas_scale;  /* observation scale (reference 10, utilities.py:107) */
+  double meas_dx;     /* trapz spacing x[2]-x[1] of the interior centres (utilities.py:91) */
+  int32_t max_iter;   /* CFL mode: step cap; a chain that hits it is invalid (Φ = +inf) */
+  int32_t reserved;
+} ipmc_model;
+
+/* One launch of n_steps pCN steps for n_chains chains. */
+typedef struct ipmc_sweep {
+  int32_t dtype;            /* ipmc_dtype of u/phi/y/gamma_inv/prior_sqrt/box_* */
+  int32_t lanes_per_chain;  /* 0 = auto; otherwise a divisor of the state dim (kernel layout only: results are identical) */
+  int64_t n_chains;
+  int64_t chain_offset;     /* global id of chain 0 of this shard (RNG counter) */
+  void* u;                  /* [n_chains, k] in/out current state */
+  void* phi;                /* [n_chains] in/out cached Φ(u) */
+  int64_t* accepts;         /* [n_chains] in/out accept counters (may be NULL) */
+  int64_t* calls;           /* [n_chains] in/out count of proposals that passed the box (may be NULL);
+                               = the inner CountedAccepter's calls under ConstrainAccepter(CountedAccepter(..)) */
+  const void* y;            /* [q] data */
+  const void* gamma_inv;    /* [q] 1/γ_i, diagonal noise covariance Γ = diag(γ²) */
+  const void* prior_sqrt;   /* [k] sqrt of the diagonal prior covariance */
+  const void* box_lo;       /* [k] or NULL: ConstrainAccepter box, valid iff lo < v+off < hi for all i */
+  const void* box_hi;       /* [k] or NULL */
+  const void* box_off;      /* [k] or NULL (treated as 0) */
+  double beta;              /* pCN step size, 0 <= beta <= 1 */
+  double contraction;       /* sqrt(1 - beta^2), computed by the host (proposer.py:77) */
+  const double* beta_schedule; /* optional [n_steps][2] (beta, contraction) of each step of this launch,
+                                  overriding beta/contraction (VarSteppCNProposer, proposer.py:110-115) */
+  uint64_t seed;            /* Philox key */
+  uint64_t step0;           /* global pCN step index of the first step of this launch */
+  int64_t n_steps;          /* pCN steps in this launch */
+  void* sample_out;         /* optional [n_chains, *] : u after the last step, row stride sample_stride elements */
+  int64_t sample_stride;
+  double* sum_u;            /* optional [n_chains, k] running sum of u after every step (f64) */
+  double* sum_u2;           /* optional [n_chains, k] running sum of u^2 */
+} ipmc_sweep;
+
+/* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */
+int ipmc_pcn_sweep(const ipmc_model* model, const ipmc_sweep* sweep, void* stream);
+
+/* Φ(u) for n parameter vectors u [n, k] -> phi [n]  (EvolutionPotential.__call__ minus the constant). */
+int ipmc_potential(const ipmc_model* model, int32_t dtype, int64_t n, const void* u,
+                   const void* y, const void* gamma_inv, void* phi, void* stream);
+
+/* G(u) for n parameter vectors u [n, k] -> g [n, q]. */
+int ipmc_forward(const ipmc_model* model, int32_t dtype, int64_t n, const void* u, void* g,
+                 void* stream);
+
+/* The proposal's standard normals: out[c, i] = ξ(seed, chain_offset + c, step, i), [n_chains, k]. */
+int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, int32_t k,
+                int32_t dtype, void* out, void* stream);
+
+/* The accept uniforms: out[c] = r(seed, chain_offset + c, step) in [0,1), always double. */
+int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out,
+                 void* stream);
+
+/* Lanes per chain the sweep kernel would use for this model/dtype when lanes_per_chain = 0. */
+int ipmc_auto_lanes(const ipmc_model* model, int32_t dtype, int64_t n_chains);
+
+const char* ipmc_last_error(void);
+int ipmc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPMC_H */

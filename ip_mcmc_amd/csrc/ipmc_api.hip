@@ -1,0 +1,258 @@
+// libipmc.so — C-ABI entry points (include/ipmc.h): argument checks, kernel
+// choice and launch.  Small-state models (linear, Lorenz-63) and the RNG
+// probes live here; Lorenz-96 and Burgers in their own translation units.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "ipmc_internal.hpp"
+#include "ipmc_small.hpp"
+
+namespace ipmc {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return IPMC_ERR_DEVICE;
+  }
+  return IPMC_OK;
+}
+
+static int fail(int code, const char* msg) {
+  set_error("%s", msg);
+  return code;
+}
+
+static int check_model(const ipmc_model* m) {
+  if (!m) return fail(IPMC_ERR_INVALID, "model is NULL");
+  if (m->k <= 0 || m->q <= 0) return fail(IPMC_ERR_INVALID, "model k and q must be positive");
+  if (!m->theta0) return fail(IPMC_ERR_INVALID, "model theta0 is NULL");
+  if (m->arith != IPMC_ARITH_FMA && m->arith != IPMC_ARITH_REFERENCE) return fail(IPMC_ERR_INVALID, "bad arith");
+  switch (m->kind) {
+    case IPMC_MODEL_LINEAR:
+      if (!m->A) return fail(IPMC_ERR_INVALID, "linear model: A is NULL");
+      if (m->k > kSmallKMax) return fail(IPMC_ERR_UNSUPPORTED, "linear model: k > 64");
+      return IPMC_OK;
+    case IPMC_MODEL_LORENZ63:
+      if (m->k != 3 || m->q != 6) return fail(IPMC_ERR_INVALID, "Lorenz-63: k must be 3 and q 6");
+      if (!m->x0 || m->n_steps <= 0) return fail(IPMC_ERR_INVALID, "Lorenz-63: x0 / n_steps");
+      return IPMC_OK;
+    case IPMC_MODEL_LORENZ96:
+      if (m->dim != m->k || m->q != m->dim) return fail(IPMC_ERR_INVALID, "Lorenz-96: k and q must equal dim");
+      if (!m->x0 || m->n_steps <= 0) return fail(IPMC_ERR_INVALID, "Lorenz-96: x0 / n_steps");
+      return IPMC_OK;
+    case IPMC_MODEL_BURGERS:
+      if (m->k != 3 || m->q != m->n_windows || !m->win_lo || !m->win_hi || !m->x0 || m->dim < 2)
+        return fail(IPMC_ERR_INVALID, "Burgers: k must be 3, q == n_windows, windows/centres set");
+      return IPMC_OK;
+  }
+  return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
+}
+
+static bool l96_has(int D, int dtype, int lpc) {
+  return dtype == IPMC_F64 ? l96_has_f64(D, lpc) : l96_has_f32(D, lpc);
+}
+
+// Smallest lane count that puts >= 2 waves on every SIMD (1024 SIMDs on
+// MI355X: 131072 lanes), else the largest compiled one.
+static int l96_auto(int D, int dtype, int64_t n_chains) {
+  static const int cands[5] = {1, 2, 4, 8, 16};
+  int best = 0;
+  for (int i = 0; i < 5; ++i) {
+    if (!l96_has(D, dtype, cands[i])) continue;
+    best = cands[i];
+    if (n_chains * cands[i] >= 131072) return cands[i];
+  }
+  return best;
+}
+
+template <typename T, int MODEL, bool FM>
+static int small_sweep_launch(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  const int64_t blocks = (s.n_chains + kSmallBlock - 1) / kSmallBlock;
+  hipLaunchKernelGGL((small_sweep_kernel<T, MODEL, FM>), dim3((unsigned)blocks), dim3(kSmallBlock), 0, st, m, s);
+  return check_launch("small_sweep_kernel");
+}
+
+template <typename T>
+static int small_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (m.kind == IPMC_MODEL_LORENZ63)
+    return fm ? small_sweep_launch<T, IPMC_MODEL_LORENZ63, true>(m, s, st)
+              : small_sweep_launch<T, IPMC_MODEL_LORENZ63, false>(m, s, st);
+  return fm ? small_sweep_launch<T, IPMC_MODEL_LINEAR, true>(m, s, st)
+            : small_sweep_launch<T, IPMC_MODEL_LINEAR, false>(m, s, st);
+}
+
+template <typename T, int MODEL, bool FM>
+static int small_eval_launch(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv,
+                             void* out, bool phi, hipStream_t st) {
+  const int64_t blocks = (n + kSmallBlock - 1) / kSmallBlock;
+  if (phi)
+    hipLaunchKernelGGL((small_eval_kernel<T, MODEL, FM, true>), dim3((unsigned)blocks), dim3(kSmallBlock), 0, st, m,
+                       n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);
+  else
+    hipLaunchKernelGGL((small_eval_kernel<T, MODEL, FM, false>), dim3((unsigned)blocks), dim3(kSmallBlock), 0, st, m,
+                       n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);
+  return check_launch("small_eval_kernel");
+}
+
+template <typename T>
+static int small_eval(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
+                      bool phi, hipStream_t st) {
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (m.kind == IPMC_MODEL_LORENZ63)
+    return fm ? small_eval_launch<T, IPMC_MODEL_LORENZ63, true>(m, n, u, y, ginv, out, phi, st)
+              : small_eval_launch<T, IPMC_MODEL_LORENZ63, false>(m, n, u, y, ginv, out, phi, st);
+  return fm ? small_eval_launch<T, IPMC_MODEL_LINEAR, true>(m, n, u, y, ginv, out, phi, st)
+            : small_eval_launch<T, IPMC_MODEL_LINEAR, false>(m, n, u, y, ginv, out, phi, st);
+}
+
+template <typename T>
+__global__ void normal_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t step, int k, T* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * k) return;
+  const int64_t c = i / k;
+  const int j = (int)(i % k);
+  double z0, z1;
+  normal_pair(seed, (uint64_t)(c_off + c), step, (uint32_t)(j >> 1), z0, z1);
+  out[i] = (T)((j & 1) ? z1 : z0);
+}
+
+__global__ void uniform_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t step, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = accept_uniform(seed, (uint64_t)(c_off + i), step);
+}
+
+static int dispatch_eval(const ipmc_model* m, int32_t dtype, int64_t n, const void* u, const void* y,
+                         const void* ginv, void* out, bool phi, void* stream) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (dtype != IPMC_F32 && dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "dtype must be IPMC_F32 or IPMC_F64");
+  if (n < 0) return fail(IPMC_ERR_INVALID, "n must be >= 0");
+  if (n == 0) return IPMC_OK;
+  if (!u || !out) return fail(IPMC_ERR_INVALID, "u / out is NULL");
+  if (phi && (!y || !ginv)) return fail(IPMC_ERR_INVALID, "y / gamma_inv is NULL");
+  hipStream_t st = (hipStream_t)stream;
+  switch (m->kind) {
+    case IPMC_MODEL_LINEAR:
+    case IPMC_MODEL_LORENZ63:
+      return dtype == IPMC_F64 ? small_eval<double>(*m, n, u, y, ginv, out, phi, st)
+                               : small_eval<float>(*m, n, u, y, ginv, out, phi, st);
+    case IPMC_MODEL_LORENZ96: {
+      const int lpc = l96_auto(m->dim, dtype, n);
+      if (!lpc) return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: no kernel compiled for this dim");
+      return dtype == IPMC_F64 ? l96_eval_f64(*m, n, u, y, ginv, out, phi, lpc, st)
+                               : l96_eval_f32(*m, n, u, y, ginv, out, phi, lpc, st);
+    }
+    case IPMC_MODEL_BURGERS:
+      return burgers_eval(*m, dtype, n, u, y, ginv, out, phi, st);
+  }
+  return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
+}
+
+}  // namespace ipmc
+
+using namespace ipmc;
+
+extern "C" {
+
+int ipmc_abi_version(void) { return IPMC_ABI_VERSION; }
+
+const char* ipmc_last_error(void) { return g_err; }
+
+int ipmc_auto_lanes(const ipmc_model* m, int32_t dtype, int64_t n_chains) {
+  if (!m) return 0;
+  if (m->kind == IPMC_MODEL_LORENZ96) return l96_auto(m->dim, dtype, n_chains);
+  return 1;
+}
+
+int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (!s) return fail(IPMC_ERR_INVALID, "sweep is NULL");
+  if (s->dtype != IPMC_F32 && s->dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "dtype must be IPMC_F32/F64");
+  if (!(s->beta >= 0.0 && s->beta <= 1.0)) return fail(IPMC_ERR_INVALID, "beta has to be in [0,1]");
+  if (s->n_chains < 0 || s->n_steps < 0 || s->chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (s->n_chains == 0 || s->n_steps == 0) {
+    if (s->n_chains > 0 && s->sample_out) {
+      // no step: the sample is the current state
+      const size_t es = s->dtype == IPMC_F64 ? 8 : 4;
+      hipStream_t st = (hipStream_t)stream;
+      if (hipMemcpy2DAsync(s->sample_out, (size_t)s->sample_stride * es, s->u, (size_t)m->k * es,
+                           (size_t)m->k * es, (size_t)s->n_chains, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return fail(IPMC_ERR_DEVICE, "sample copy failed");
+    }
+    return IPMC_OK;
+  }
+  if (!s->u || !s->phi || !s->y || !s->gamma_inv || !s->prior_sqrt)
+    return fail(IPMC_ERR_INVALID, "u / phi / y / gamma_inv / prior_sqrt is NULL");
+  if (s->sample_out && s->sample_stride < m->k) return fail(IPMC_ERR_INVALID, "sample_stride < k");
+  if (s->sum_u2 && !s->sum_u) return fail(IPMC_ERR_INVALID, "sum_u2 needs sum_u");
+  hipStream_t st = (hipStream_t)stream;
+  switch (m->kind) {
+    case IPMC_MODEL_LINEAR:
+    case IPMC_MODEL_LORENZ63:
+      if (s->lanes_per_chain > 1) return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane");
+      return s->dtype == IPMC_F64 ? small_sweep<double>(*m, *s, st) : small_sweep<float>(*m, *s, st);
+    case IPMC_MODEL_LORENZ96: {
+      int lpc = s->lanes_per_chain;
+      if (lpc == 0) lpc = l96_auto(m->dim, s->dtype, s->n_chains);
+      if (!lpc || !l96_has(m->dim, s->dtype, lpc)) {
+        set_error("Lorenz-96: no kernel compiled for dim=%d lanes_per_chain=%d", m->dim, lpc);
+        return IPMC_ERR_UNSUPPORTED;
+      }
+      return s->dtype == IPMC_F64 ? l96_sweep_f64(*m, *s, lpc, st) : l96_sweep_f32(*m, *s, lpc, st);
+    }
+    case IPMC_MODEL_BURGERS:
+      return burgers_sweep(*m, *s, st);
+  }
+  return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
+}
+
+int ipmc_potential(const ipmc_model* m, int32_t dtype, int64_t n, const void* u, const void* y,
+                   const void* gamma_inv, void* phi, void* stream) {
+  return dispatch_eval(m, dtype, n, u, y, gamma_inv, phi, true, stream);
+}
+
+int ipmc_forward(const ipmc_model* m, int32_t dtype, int64_t n, const void* u, void* g, void* stream) {
+  return dispatch_eval(m, dtype, n, u, nullptr, nullptr, g, false, stream);
+}
+
+int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, int32_t k, int32_t dtype,
+                void* out, void* stream) {
+  if (n_chains < 0 || k < 0 || chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (dtype != IPMC_F32 && dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "bad dtype");
+  const int64_t total = n_chains * k;
+  if (total == 0) return IPMC_OK;
+  if (!out) return fail(IPMC_ERR_INVALID, "out is NULL");
+  const int64_t blocks = (total + 255) / 256;
+  if (dtype == IPMC_F64)
+    hipLaunchKernelGGL(normal_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, seed,
+                       chain_offset, n_chains, step, k, (double*)out);
+  else
+    hipLaunchKernelGGL(normal_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, seed,
+                       chain_offset, n_chains, step, k, (float*)out);
+  return check_launch("normal_kernel");
+}
+
+int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out, void* stream) {
+  if (n_chains < 0 || chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (n_chains == 0) return IPMC_OK;
+  if (!out) return fail(IPMC_ERR_INVALID, "out is NULL");
+  const int64_t blocks = (n_chains + 255) / 256;
+  hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, seed, chain_offset,
+                     n_chains, step, out);
+  return check_launch("uniform_kernel");
+}
+
+}  // extern "C"

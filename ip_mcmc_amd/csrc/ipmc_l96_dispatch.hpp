@@ -1,0 +1,119 @@
+// Lorenz-96 instantiation table and launchers (included by ipmc_l96_f32.hip
+// and ipmc_l96_f64.hip, one dtype per translation unit so they build in parallel).
+#pragma once
+
+#include "ipmc_internal.hpp"
+#include "ipmc_l96.hpp"
+
+namespace ipmc {
+
+// State dims with a compiled kernel. Each (D, LPC) needs M = D/LPC >= 2
+// components per lane and at most 160 B of state per lane-array (6 arrays of
+// M live in VGPRs).
+#define IPMC_L96_DIMS(X) X(4) X(8) X(16) X(20) X(32) X(36) X(40) X(64) X(128) X(256)
+
+template <typename T, int D, int LPC>
+constexpr bool l96_ok() {
+  return LPC <= 16 && D % LPC == 0 && D / LPC >= 2 && (D / LPC) * (int)sizeof(T) <= 160;
+}
+
+template <typename T, int D, int LPC, bool FM>
+int l96_launch_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  const int64_t threads = s.n_chains * LPC;
+  const int64_t blocks = (threads + kL96Block - 1) / kL96Block;
+  hipLaunchKernelGGL((l96_sweep_kernel<T, D, LPC, FM>), dim3((unsigned)blocks), dim3(kL96Block), 0, st, m, s);
+  return check_launch("l96_sweep_kernel");
+}
+
+template <typename T, int D, int LPC, bool FM>
+int l96_launch_eval(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
+                    bool phi, hipStream_t st) {
+  const int64_t threads = n * LPC;
+  const int64_t blocks = (threads + kL96Block - 1) / kL96Block;
+  if (phi)
+    hipLaunchKernelGGL((l96_eval_kernel<T, D, LPC, FM, true>), dim3((unsigned)blocks), dim3(kL96Block), 0, st, m, n,
+                       (const T*)u, (const T*)y, (const T*)ginv, (T*)out);
+  else
+    hipLaunchKernelGGL((l96_eval_kernel<T, D, LPC, FM, false>), dim3((unsigned)blocks), dim3(kL96Block), 0, st, m,
+                       n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);
+  return check_launch("l96_eval_kernel");
+}
+
+template <typename T, int D, bool FM>
+int l96_sweep_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+  switch (lpc) {
+#define IPMC_CASE(L)                                                                   \
+  case L:                                                                              \
+    if constexpr (l96_ok<T, D, L>()) return l96_launch_sweep<T, D, L, FM>(m, s, st); \
+    break;
+    IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
+#undef IPMC_CASE
+  }
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+template <typename T, int D, bool FM>
+int l96_eval_d(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
+               int lpc, hipStream_t st) {
+  switch (lpc) {
+#define IPMC_CASE(L)                                                                                  \
+  case L:                                                                                             \
+    if constexpr (l96_ok<T, D, L>()) return l96_launch_eval<T, D, L, FM>(m, n, u, y, ginv, out, phi, st); \
+    break;
+    IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
+#undef IPMC_CASE
+  }
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int l96_sweep_t(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+  const bool fm = (m.arith == IPMC_ARITH_FMA);
+  switch (m.dim) {
+#define IPMC_DIM(D) \
+  case D: return fm ? l96_sweep_d<T, D, true>(m, s, lpc, st) : l96_sweep_d<T, D, false>(m, s, lpc, st);
+    IPMC_L96_DIMS(IPMC_DIM)
+#undef IPMC_DIM
+  }
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int l96_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
+               int lpc, hipStream_t st) {
+  const bool fm = (m.arith == IPMC_ARITH_FMA);
+  switch (m.dim) {
+#define IPMC_DIM(D)                                                                  \
+  case D:                                                                            \
+    return fm ? l96_eval_d<T, D, true>(m, n, u, y, ginv, out, phi, lpc, st)          \
+              : l96_eval_d<T, D, false>(m, n, u, y, ginv, out, phi, lpc, st);
+    IPMC_L96_DIMS(IPMC_DIM)
+#undef IPMC_DIM
+  }
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+template <typename T, int D>
+bool l96_has_d(int lpc) {
+  switch (lpc) {
+    case 1: return l96_ok<T, D, 1>();
+    case 2: return l96_ok<T, D, 2>();
+    case 4: return l96_ok<T, D, 4>();
+    case 8: return l96_ok<T, D, 8>();
+    case 16: return l96_ok<T, D, 16>();
+  }
+  return false;
+}
+
+template <typename T>
+bool l96_has_t(int D, int lpc) {
+  switch (D) {
+#define IPMC_DIM(DD) \
+  case DD: return l96_has_d<T, DD>(lpc);
+    IPMC_L96_DIMS(IPMC_DIM)
+#undef IPMC_DIM
+  }
+  return false;
+}
+
+}  // namespace ipmc

@@ -1,0 +1,15 @@
+// Lorenz-96 kernels, fp64 instantiations.
+#include "ipmc_l96_dispatch.hpp"
+
+namespace ipmc {
+
+int l96_sweep_f64(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+  return l96_sweep_t<double>(m, s, lpc, st);
+}
+int l96_eval_f64(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
+                 int lpc, hipStream_t st) {
+  return l96_eval_t<double>(m, n, u, y, ginv, out, phi, lpc, st);
+}
+bool l96_has_f64(int D, int lpc) { return l96_has_t<double>(D, lpc); }
+
+}  // namespace ipmc

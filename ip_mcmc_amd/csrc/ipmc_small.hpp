@@ -1,0 +1,175 @@
+// Small-state forward maps, one chain per lane (LPC = 1):
+//   LINEAR    G(u) = A (theta0 + u)                    stuart_examples.py:69-70
+//   LORENZ63  RK4 Lorenz-63, theta = (sigma, rho, b) = theta0 + u, observations the
+//             time averages of (x, y, z, x^2, y^2, z^2) (lorenz_mcmc.py:17-40 pattern)
+#pragma once
+
+#include "ipmc_sweep_common.hpp"
+
+namespace ipmc {
+
+constexpr int kSmallBlock = 64;
+constexpr int kSmallKMax = 64;  // linear: k <= 64 (proposal parked in LDS)
+
+template <typename T, bool FM>
+__device__ __forceinline__ void l63_rhs(T sg, T rh, T bb, const T (&s)[3], T (&o)[3]) {
+  if constexpr (FM) {
+    o[0] = sg * (s[1] - s[0]);
+    o[1] = madd<true>(s[0], rh - s[2], -s[1]);
+    o[2] = madd<true>(s[0], s[1], -(bb * s[2]));
+  } else {
+    o[0] = sg * (s[1] - s[0]);
+    o[1] = s[0] * (rh - s[2]) - s[1];
+    o[2] = s[0] * s[1] - bb * s[2];
+  }
+}
+
+template <typename T, bool FM>
+__device__ __forceinline__ void l63_forward(T sg, T rh, T bb, const T* __restrict__ x0, T h, int nsteps, T (&g)[6]) {
+  const T h2 = h * (T)0.5, h6 = h / (T)6;
+  T x[3] = {x0[0], x0[1], x0[2]};
+  T ob[6] = {0, 0, 0, 0, 0, 0};
+  for (int n = 0; n < nsteps; ++n) {
+    T k1[3], k2[3], k3[3], k4[3], xs[3];
+    l63_rhs<T, FM>(sg, rh, bb, x, k1);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xs[i] = madd<FM>(h2, k1[i], x[i]);
+    l63_rhs<T, FM>(sg, rh, bb, xs, k2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xs[i] = madd<FM>(h2, k2[i], x[i]);
+    l63_rhs<T, FM>(sg, rh, bb, xs, k3);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) xs[i] = madd<FM>(h, k3[i], x[i]);
+    l63_rhs<T, FM>(sg, rh, bb, xs, k4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const T a = ((k1[i] + (T)2 * k2[i]) + (T)2 * k3[i]) + k4[i];
+      x[i] = madd<FM>(h6, a, x[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      ob[i] = ob[i] + x[i];
+      ob[3 + i] = madd<FM>(x[i], x[i], ob[3 + i]);
+    }
+  }
+  const T nn = (T)nsteps;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) g[i] = ob[i] / nn;
+}
+
+// Φ for the lane's chain; v is read from the LDS park (column `col`).
+template <typename T, int MODEL, bool FM>
+__device__ __forceinline__ T small_potential(const ipmc_model& m, const T* __restrict__ v, int vstride,
+                                             const T* __restrict__ y, const T* __restrict__ ginv) {
+  const T* th0 = (const T*)m.theta0;
+  T s = (T)0;
+  if constexpr (MODEL == IPMC_MODEL_LORENZ63) {
+    T g[6];
+    l63_forward<T, FM>(th0[0] + v[0], th0[1] + v[vstride], th0[2] + v[2 * vstride], (const T*)m.x0, (T)m.dt,
+                       m.n_steps, g);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const T r = (y[i] - g[i]) * ginv[i];
+      s = madd<FM>(r, r, s);
+    }
+  } else {
+    const T* A = (const T*)m.A;
+    const int k = m.k;
+    for (int i = 0; i < m.q; ++i) {
+      T acc = (T)0;
+      for (int j = 0; j < k; ++j) acc = madd<FM>(A[(int64_t)i * k + j], th0[j] + v[j * vstride], acc);
+      const T r = (y[i] - acc) * ginv[i];
+      s = madd<FM>(r, r, s);
+    }
+  }
+  return (T)0.5 * s;
+}
+
+template <typename T, int MODEL, bool FM>
+__global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
+  __shared__ T vpark[kSmallKMax * kSmallBlock];
+  const int64_t chain = (int64_t)blockIdx.x * kSmallBlock + threadIdx.x;
+  if (chain >= s.n_chains) return;
+  const int k = m.k;
+  const uint64_t gid = (uint64_t)(s.chain_offset + chain);
+  T* __restrict__ u = (T*)s.u + chain * k;
+  const T* sq = (const T*)s.prior_sqrt;
+  const T* lo = (const T*)s.box_lo;
+  const T* hi = (const T*)s.box_hi;
+  const T* off = (const T*)s.box_off;
+  const T beta = (T)s.beta, contr = (T)s.contraction;
+  T* phi = (T*)s.phi;
+  T* v = vpark + threadIdx.x;  // v[j * kSmallBlock]
+  T phu = phi[chain];
+  int64_t nacc = 0, ncalls = 0;
+  for (int64_t st = 0; st < s.n_steps; ++st) {
+    const uint64_t step = s.step0 + (uint64_t)st;
+    const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
+    const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
+    double z0 = 0.0, z1 = 0.0;
+    bool ok = true;
+    for (int j = 0; j < k; ++j) {
+      if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+      const T w = sq[j] * (T)((j & 1) ? z1 : z0);
+      const T vj = cs * u[j] + bs * w;
+      v[j * kSmallBlock] = vj;
+      const T t = vj + (off ? off[j] : (T)0);
+      if (lo && !(lo[j] < t)) ok = false;
+      if (hi && !(t < hi[j])) ok = false;
+    }
+    if (ok) {
+      ++ncalls;
+      const T phv =
+          small_potential<T, MODEL, FM>(m, v, kSmallBlock, (const T*)s.y, (const T*)s.gamma_inv);
+      if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
+        for (int j = 0; j < k; ++j) u[j] = v[j * kSmallBlock];
+        phu = phv;
+        ++nacc;
+      }
+    }
+    if (s.sum_u) {
+      for (int j = 0; j < k; ++j) {
+        const double ud = (double)u[j];
+        s.sum_u[chain * k + j] += ud;
+        if (s.sum_u2) s.sum_u2[chain * k + j] += ud * ud;
+      }
+    }
+  }
+  phi[chain] = phu;
+  if (s.accepts) s.accepts[chain] += nacc;
+  if (s.calls) s.calls[chain] += ncalls;
+  if (s.sample_out) {
+    T* so = (T*)s.sample_out + chain * s.sample_stride;
+    for (int j = 0; j < k; ++j) so[j] = u[j];
+  }
+}
+
+template <typename T, int MODEL, bool FM, bool PHI>
+__global__ __launch_bounds__(kSmallBlock) void small_eval_kernel(const ipmc_model m, int64_t n,
+                                                                 const T* __restrict__ uin,
+                                                                 const T* __restrict__ y,
+                                                                 const T* __restrict__ ginv, T* __restrict__ out) {
+  const int64_t chain = (int64_t)blockIdx.x * kSmallBlock + threadIdx.x;
+  if (chain >= n) return;
+  const T* v = uin + chain * m.k;
+  if constexpr (PHI) {
+    out[chain] = small_potential<T, MODEL, FM>(m, v, 1, y, ginv);
+  } else {
+    const T* th0 = (const T*)m.theta0;
+    if constexpr (MODEL == IPMC_MODEL_LORENZ63) {
+      T g[6];
+      l63_forward<T, FM>(th0[0] + v[0], th0[1] + v[1], th0[2] + v[2], (const T*)m.x0, (T)m.dt, m.n_steps, g);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) out[chain * 6 + i] = g[i];
+    } else {
+      const T* A = (const T*)m.A;
+      for (int i = 0; i < m.q; ++i) {
+        T acc = (T)0;
+        for (int j = 0; j < m.k; ++j) acc = madd<FM>(A[(int64_t)i * m.k + j], th0[j] + v[j], acc);
+        out[chain * m.q + i] = acc;
+      }
+    }
+  }
+}
+
+}  // namespace ipmc

@@ -1,0 +1,73 @@
+"""Device plumbing: torch tensors for HBM buffers, the current HIP stream, and
+thin wrappers over the libipmc entry points that are not the sweep itself.
+
+PyTorch is used only for memory, streams and torch.distributed; all compute is
+libipmc's HIP kernels.
+"""
+import numpy as np
+import torch
+
+from . import _abi
+from ._lib import call
+
+F32 = torch.float32
+F64 = torch.float64
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("ip_mcmc_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+
+
+def resolve_device(device=None):
+    require_gpu()
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"device must be a cuda (ROCm) device, got {d}")
+    if d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+def torch_dtype(dtype):
+    if dtype in (None, np.float64, "float64", "f64", torch.float64, float):
+        return F64
+    if dtype in (np.float32, "float32", "f32", torch.float32):
+        return F32
+    raise ValueError(f"unsupported dtype {dtype!r} (float32 or float64)")
+
+
+def abi_dtype(tdtype):
+    return _abi.F64 if tdtype == F64 else _abi.F32
+
+
+def stream_handle(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def to_device(x, dtype, device):
+    """numpy / list / tensor -> contiguous tensor of `dtype` on `device`."""
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.asarray(x, dtype=np.float64), dtype=dtype).to(device).contiguous()
+
+
+def normals(seed, chain_offset, n_chains, step, k, dtype=None, device=None):
+    device = resolve_device(device)
+    td = torch_dtype(dtype)
+    out = torch.empty((n_chains, k), dtype=td, device=device)
+    call("ipmc_normal", seed, chain_offset, n_chains, step, k, abi_dtype(td), ptr(out), stream_handle(device))
+    return out
+
+
+def uniforms(seed, chain_offset, n_chains, step, device=None):
+    device = resolve_device(device)
+    out = torch.empty((n_chains,), dtype=F64, device=device)
+    call("ipmc_uniform", seed, chain_offset, n_chains, step, ptr(out), stream_handle(device))
+    return out

@@ -1,0 +1,64 @@
+"""pCN proposers — mirror of ``ip_mcmc/proposer.py`` (the pCN part).
+
+v = sqrt(1 − β²)·u + β·w,  w ~ N(0, C)   (Cotter et al. 2013 eq. 4.8)
+
+The device path draws w = sqrt(C_ii)·ξ_i from the counter-based stream
+(rng.py) inside the sweep kernel; ``__call__`` keeps the reference's
+single-step host signature for API compatibility.
+"""
+from abc import ABC, abstractmethod
+
+import numpy as np
+
+from .distribution import GaussianDistribution
+
+
+class ProposerBase(ABC):
+    """proposer.py:8-11."""
+
+    @abstractmethod
+    def __call__(self, u, rng):
+        ...
+
+
+class ConstSteppCNProposer(ProposerBase):
+    """proposer.py:59-82.  Only the prior covariance is used; a non-zero prior
+    mean is ignored (callers sample perturbations around it, Q1)."""
+
+    def __init__(self, beta, prior):
+        assert 0 <= beta <= 1, "beta has to be in [0,1]"
+        self.beta = beta
+        self.contraction = np.sqrt(1 - beta**2)  # proposer.py:77
+        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+
+    def beta_schedule(self, i0, n):
+        """(beta, contraction) for proposals i0+1 .. i0+n (constant here)."""
+        return None
+
+    def __call__(self, u, rng):
+        return self.contraction * u + self.beta * self.w.sample(rng)
+
+
+class VarSteppCNProposer(ProposerBase):
+    """proposer.py:85-115: beta(i) for the i-th proposal, i counted from 1
+    (incremented before use, :111-112).  The sampler passes the schedule of
+    each launch to the kernel (ipmc_sweep.beta_schedule)."""
+
+    def __init__(self, beta, prior):
+        self.beta = beta
+        self.i = 0
+        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+
+    def beta_schedule(self, i0, n):
+        b = np.array([float(self.beta(i0 + j + 1)) for j in range(n)], dtype=np.float64)
+        if np.any((b < 0) | (b > 1)):
+            raise ValueError("beta(i) has to be in [0,1]")
+        sched = np.empty((n, 2), dtype=np.float64)
+        sched[:, 0] = b
+        sched[:, 1] = np.sqrt(1 - b**2)
+        return sched
+
+    def __call__(self, u, rng):
+        self.i += 1
+        b = self.beta(self.i)
+        return np.sqrt(1 - b**2) * u + b * self.w.sample(rng)

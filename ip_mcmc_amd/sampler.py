@@ -1,0 +1,284 @@
+"""MCMCSampler — drop-in for ``ip_mcmc/sampler.py`` on many chains at once.
+
+Reference (sampler.py:6-54): ``MCMCSampler(proposal, acceptance, rng)``;
+``run(u_0, n_samples, burn_in=1000, sample_interval=200)`` advances ONE chain
+``max(0, burn_in − sample_interval) + n_samples·sample_interval`` steps
+(:18-26), records the state after every block of ``sample_interval`` steps
+(:28) and returns a float64 array (n_samples, k).
+
+Here ``u_0`` may be one state (k,) — same return shape as the reference — or
+a stack (C, k) of C independent chains, returning (C, n_samples, k).  The
+pCN step (ConstSteppCNProposer / VarSteppCNProposer + pCNAccepter on an
+EvolutionPotential with a device forward map, optionally wrapped in
+CountedAccepter / ConstrainAccepter(BoxConstraint)) runs as one fused HIP
+kernel per block of steps (libipmc ``ipmc_pcn_sweep``).  Any other
+composition raises ``UnsupportedOnDevice``: there is no CPU fallback.
+
+Differences from the reference, all deliberate:
+  * randomness is the counter-based Philox stream of rng.py, not PCG64;
+  * Φ(u) is cached between steps instead of recomputed (accepter.py:122);
+  * the per-sample ``print`` (sampler.py:24) happens only with verbose=True.
+"""
+import ctypes as C
+import math
+import time
+
+import numpy as np
+import torch
+
+from . import _abi
+from . import device as dev
+from ._lib import UnsupportedOnDevice, call
+from .accepter import BoxConstraint, ConstrainAccepter, CountedAccepter, pCNAccepter
+from .potential import EvolutionPotential
+from .proposer import ConstSteppCNProposer, VarSteppCNProposer
+from .rng import PhiloxRNG, resolve_rng
+
+# pCN steps per chain in one kernel launch (launches are split at sample
+# boundaries; this bounds a single launch's run time for large ensembles).
+STEPS_PER_LAUNCH = 1024
+
+
+class _Plan:
+    """The device form of a proposer/accepter composition."""
+
+    def __init__(self, proposer, accepter):
+        if not isinstance(proposer, (ConstSteppCNProposer, VarSteppCNProposer)):
+            raise UnsupportedOnDevice(
+                f"device sampler needs a ConstSteppCNProposer or VarSteppCNProposer, not {type(proposer).__name__}"
+            )
+        if not proposer.w.is_diagonal:
+            raise UnsupportedOnDevice("device sampler needs a diagonal prior covariance")
+        self.proposer = proposer
+        self.prior_sqrt = proposer.w.sqrt_diagonal
+        self.counted_outer = []  # CountedAccepters that see every step
+        self.counted_inner = []  # CountedAccepters inside a ConstrainAccepter
+        self.box = None
+        acc, inside = accepter, False
+        while True:
+            if isinstance(acc, CountedAccepter):
+                (self.counted_inner if inside else self.counted_outer).append(acc)
+                acc = acc.accepter
+            elif isinstance(acc, ConstrainAccepter):
+                if self.box is not None:
+                    raise UnsupportedOnDevice("only one ConstrainAccepter is supported on the device")
+                if not isinstance(acc.is_valid, BoxConstraint):
+                    raise UnsupportedOnDevice(
+                        "ConstrainAccepter on the device needs a BoxConstraint (a Python callable cannot run in the kernel)"
+                    )
+                self.box = acc.is_valid
+                inside = True
+                acc = acc.accepter
+            elif isinstance(acc, pCNAccepter):
+                break
+            else:
+                raise UnsupportedOnDevice(f"device sampler needs a pCNAccepter, not {type(acc).__name__}")
+        pot = acc.theta
+        if not isinstance(pot, EvolutionPotential):
+            raise UnsupportedOnDevice(f"pCNAccepter on the device needs an EvolutionPotential, not {type(pot).__name__}")
+        self.potential = pot
+        self.G = pot.G
+        self.y_eff, self.gamma_inv = pot.device_terms()
+        if self.prior_sqrt.shape[0] != self.G.k:
+            raise ValueError(f"prior dimension {self.prior_sqrt.shape[0]} != forward map k = {self.G.k}")
+
+
+class MCMCSampler:
+    def __init__(
+        self,
+        proposal,
+        acceptance,
+        rng,
+        dtype=np.float64,
+        device=None,
+        lanes_per_chain=0,
+        chain_offset=0,
+        verbose=False,
+    ):
+        self.proposer = proposal
+        self.accepter = acceptance
+        self.rng = rng
+        self.dtype = dtype
+        self.device = device
+        self.lanes_per_chain = int(lanes_per_chain)
+        self.chain_offset = int(chain_offset)
+        self.verbose = verbose
+        # state of the last run (device tensors), for inspection / continuation
+        self.state = None
+        self.last_run_seconds = None
+
+    # ------------------------------------------------------------------ run
+    def run(self, u_0, n_samples, burn_in=1000, sample_interval=200, keep="samples"):
+        """Run the chain(s).  keep='samples' returns the samples like the
+        reference; keep='moments' returns a dict of per-chain sums of u and u²
+        over every post-burn-in step (no sample array); keep='last' returns
+        the final states (C, k)."""
+        if keep not in ("samples", "moments", "last"):
+            raise ValueError("keep must be 'samples', 'moments' or 'last'")
+        plan = _Plan(self.proposer, self.accepter)
+        device = dev.resolve_device(self.device)
+        td = dev.torch_dtype(self.dtype)
+        k = plan.G.k
+        if isinstance(u_0, torch.Tensor):
+            single = u_0.dim() <= 1
+            U = u_0.reshape(-1, k).to(device=device, dtype=td).clone().contiguous()
+        else:
+            arr = np.asarray(u_0, dtype=np.float64)
+            single = arr.ndim <= 1
+            U = dev.to_device(arr.reshape(-1, k), td, device).clone()
+        n_chains = U.shape[0]
+        n_samples = int(n_samples)
+        sample_interval = int(sample_interval)
+        if n_samples < 0 or sample_interval < 0:
+            raise ValueError("n_samples and sample_interval must be >= 0")
+
+        rng = resolve_rng(self.rng)
+        if isinstance(self.accepter, CountedAccepter):
+            self.accepter.reset()  # sampler.py:15-16
+
+        stream = dev.stream_handle(device)
+        phi = plan.potential.phi_device(U)
+        accepts = torch.zeros((n_chains,), dtype=torch.int64, device=device)
+        calls = torch.zeros((n_chains,), dtype=torch.int64, device=device) if plan.counted_inner else None
+        y_t = dev.to_device(plan.y_eff, td, device)
+        gi_t = dev.to_device(plan.gamma_inv, td, device)
+        sq_t = dev.to_device(plan.prior_sqrt, td, device)
+        keep_alive = [y_t, gi_t, sq_t]
+        box_ptrs = (None, None, None)
+        if plan.box is not None:
+            arrs = plan.box.arrays(k)
+            ts = [None if a is None else dev.to_device(a, td, device) for a in arrs]
+            keep_alive += [t for t in ts if t is not None]
+            box_ptrs = tuple(dev.ptr(t) for t in ts)
+        model, _ = plan.G.model(td, device)
+
+        sw = _abi.IpmcSweep()
+        sw.dtype = dev.abi_dtype(td)
+        sw.lanes_per_chain = self.lanes_per_chain
+        sw.n_chains = n_chains
+        sw.chain_offset = self.chain_offset
+        sw.u = U.data_ptr()
+        sw.phi = phi.data_ptr()
+        sw.accepts = accepts.data_ptr()
+        sw.calls = dev.ptr(calls)
+        sw.y = y_t.data_ptr()
+        sw.gamma_inv = gi_t.data_ptr()
+        sw.prior_sqrt = sq_t.data_ptr()
+        sw.box_lo, sw.box_hi, sw.box_off = box_ptrs
+        const_beta = isinstance(plan.proposer, ConstSteppCNProposer)
+        if const_beta:
+            sw.beta = float(plan.proposer.beta)
+            sw.contraction = float(plan.proposer.contraction)
+        sw.seed = rng.seed
+
+        step = rng.step
+        prop_i = getattr(plan.proposer, "i", 0)
+
+        def launch(n, sample_view=None, sums=None):
+            nonlocal step, prop_i
+            if n <= 0 and sample_view is None:
+                return
+            sched = None
+            if not const_beta and n > 0:
+                sched = torch.as_tensor(plan.proposer.beta_schedule(prop_i, n)).to(device)
+                keep_alive.append(sched)
+            sw.beta_schedule = dev.ptr(sched)
+            if not const_beta:
+                sw.beta, sw.contraction = 0.0, 1.0
+            sw.step0 = step
+            sw.n_steps = n
+            if sample_view is not None:
+                sw.sample_out = sample_view.data_ptr()
+                sw.sample_stride = sample_view.stride(0)
+            else:
+                sw.sample_out = None
+                sw.sample_stride = 0
+            sw.sum_u, sw.sum_u2 = (None, None) if sums is None else (sums[0].data_ptr(), sums[1].data_ptr())
+            call("ipmc_pcn_sweep", C.byref(model), C.byref(sw), stream)
+            step += n
+            prop_i += n
+
+        t0 = time.perf_counter()
+        n_burn = max(0, burn_in - sample_interval)  # sampler.py:18
+        for c0 in range(0, n_burn, STEPS_PER_LAUNCH):
+            launch(min(STEPS_PER_LAUNCH, n_burn - c0))
+
+        samples = None
+        sums = None
+        if keep == "samples":
+            samples = torch.empty((n_chains, n_samples, k), dtype=td, device=device)
+        elif keep == "moments":
+            sums = (
+                torch.zeros((n_chains, k), dtype=torch.float64, device=device),
+                torch.zeros((n_chains, k), dtype=torch.float64, device=device),
+            )
+        for i in range(n_samples):  # sampler.py:23-28
+            if self.verbose:
+                print(f"Sampling {i + 1}/{n_samples}")
+            done = 0
+            while done < sample_interval:
+                n = min(STEPS_PER_LAUNCH, sample_interval - done)
+                last = done + n == sample_interval
+                view = samples[:, i, :] if (samples is not None and last) else None
+                launch(n, view, sums)
+                done += n
+            if sample_interval == 0 and samples is not None:
+                launch(0, samples[:, i, :])
+        torch.cuda.synchronize(device)
+        self.last_run_seconds = time.perf_counter() - t0
+
+        total = step - rng.step
+        rng.step = step
+        if isinstance(plan.proposer, VarSteppCNProposer):
+            plan.proposer.i = prop_i
+
+        acc_np = accepts.cpu().numpy()
+        calls_np = calls.cpu().numpy() if calls is not None else None
+        for ca in plan.counted_outer:
+            _bump(ca, np.full(n_chains, total, dtype=np.int64), acc_np, single)
+        for ca in plan.counted_inner:
+            _bump(ca, calls_np, acc_np, single)
+        if self.verbose and isinstance(self.accepter, CountedAccepter):
+            print(f"Acceptance ratio: {self.accepter.ratio()}")  # sampler.py:30-31
+
+        self.state = {"u": U, "phi": phi, "accepts": accepts, "calls": calls, "steps": total, "rng": rng}
+        if keep == "samples":
+            out = samples.double().cpu().numpy()
+            return out[0] if single else out
+        if keep == "moments":
+            n_post = n_samples * sample_interval
+            res = {"sum_u": sums[0].cpu().numpy(), "sum_u2": sums[1].cpu().numpy(), "n": n_post}
+            if single:
+                res = {"sum_u": res["sum_u"][0], "sum_u2": res["sum_u2"][0], "n": n_post}
+            return res
+        last = U.double().cpu().numpy()
+        return last[0] if single else last
+
+    def _step(self, u, rng):
+        """sampler.py:35-41, one host step (API compatibility; not the hot path)."""
+        v = self.proposer(u, rng)
+        if self.accepter(u, v, rng):
+            return v
+        return u
+
+    @classmethod
+    def autocorr(cls, x):
+        """Normalised autocorrelation of a 1-D chain (sampler.py:43-54)."""
+        x = np.asarray(x, dtype=np.float64)
+        x_ = x - np.mean(x)
+        result = np.correlate(x_, x_, mode="full")
+        result = result[-len(x):]
+        if result[0] == 0:
+            return np.ones_like(result)
+        return result / result[0]
+
+
+def _bump(counted, calls, accepts, single):
+    if single:
+        counted.calls = int(np.asarray(counted.calls).sum()) + int(calls[0])
+        counted.accepts = int(np.asarray(counted.accepts).sum()) + int(accepts[0])
+        return
+    c0 = np.asarray(counted.calls)
+    a0 = np.asarray(counted.accepts)
+    counted.calls = (c0 if c0.shape == calls.shape else 0) + calls
+    counted.accepts = (a0 if a0.shape == accepts.shape else 0) + accepts

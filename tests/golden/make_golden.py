@@ -1,0 +1,338 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE.
+
+Run in the build container only (needs /root/reference, which the GPU box
+does not have):   python tests/golden/make_golden.py
+
+Nothing of the reference is copied: this script imports its modules from
+/root/reference, calls them, and stores inputs and outputs as .npz data.
+
+Shims (all are name/compat fixes on the reference's own code):
+  * ``ip_mcmc.pCNProposer`` is aliased to ``ConstSteppCNProposer`` so that
+    report/scripts/lorenz.py (which imports the stale name) imports.
+  * burgers/rusanov.py is imported directly; RusanovFVM.integrate uses the
+    removed ``np.float`` (rusanov.py:32), so the harness sets the initial
+    state itself and then drives the reference's own ``_cfl`` / ``_step``
+    exactly as integrate does (rusanov.py:34-45).
+  * burgers/utilities.py is NOT imported (it imports helpers.py, which needs
+    the absent POT package); its Measurer formula (utilities.py:100-109,
+    10 * np.trapz(values[l:r], dx)) is evaluated with numpy's own trapz.
+The reference's RNG seam (test_utilities.py:11-26: a np.random.Generator
+subclass) injects the build's counter-based draws into the reference sampler.
+"""
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REF, "ip_mcmc"))
+sys.path.insert(0, os.path.join(REF, "report", "scripts"))
+sys.path.insert(0, os.path.join(REF, "report", "scripts", "burgers"))
+
+import numpy as np  # noqa: E402
+
+import matplotlib  # noqa: E402
+
+matplotlib.use("Agg")
+
+import ip_mcmc  # noqa: E402
+from ip_mcmc import (  # noqa: E402
+    ConstrainAccepter,
+    ConstSteppCNProposer,
+    CountedAccepter,
+    EvolutionPotential,
+    GaussianDistribution,
+    MCMCSampler,
+    pCNAccepter,
+)
+
+ip_mcmc.pCNProposer = ConstSteppCNProposer  # stale name in lorenz.py:8
+import lorenz  # noqa: E402  report/scripts/lorenz.py
+import rusanov  # noqa: E402  report/scripts/burgers/rusanov.py
+
+from oracle import oracle as O  # noqa: E402  (draws only: Philox stream)
+
+
+# --------------------------------------------------------------- injection
+class CounterRNG(np.random.Generator):
+    """The reference's MockRNG seam (test_utilities.py:11-26) fed with the
+    build's counter-based draws: multivariate_normal returns sqrt(C)·ξ(step)
+    and random() returns r(step) for one chain.  Each multivariate_normal call
+    starts a new step (the proposal precedes the accept draw, sampler.py:36-38)."""
+
+    def __init__(self, seed, chain, step0=0):
+        super().__init__(np.random.PCG64())
+        self.s = seed
+        self.chain = chain
+        self.step = step0 - 1
+        self.uniform_steps = []
+
+    def multivariate_normal(self, mean=None, cov=None):
+        self.step += 1
+        k = len(mean)
+        xi = O.normals(self.s, self.chain, 1, self.step, k)[0]
+        cov = np.asarray(cov)
+        assert np.all(cov == np.diag(np.diag(cov))), "harness handles diagonal covariances"
+        return np.sqrt(np.diag(cov)) * xi + mean
+
+    def random(self):
+        self.uniform_steps.append(self.step)
+        return float(O.uniforms(self.s, self.chain, 1, self.step)[0])
+
+
+class RecordingAccepter:
+    """Wraps the reference accepter and records the decision of every step."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.decisions = []
+
+    def __call__(self, u, v, rng):
+        a = self.inner(u, v, rng)
+        self.decisions.append(bool(a))
+        return a
+
+
+def run_reference_chain(G, y, noise_cov_diag, prior_var_diag, beta, u0, seed, chain, n_samples, burn_in, interval,
+                        box=None):
+    prior = GaussianDistribution(mean=np.zeros(len(u0)), covariance=np.diag(prior_var_diag))
+    noise = GaussianDistribution(mean=np.zeros(len(y)), covariance=np.diag(noise_cov_diag))
+    pot = EvolutionPotential(G, y, noise)
+    prop = ConstSteppCNProposer(beta, prior)
+    inner = CountedAccepter(pCNAccepter(pot))
+    rec = RecordingAccepter(inner)
+    acc = rec if box is None else ConstrainAccepter(rec, box)
+    rng = CounterRNG(seed, chain)
+    sampler = MCMCSampler(prop, acc, rng)
+    import contextlib
+    import io
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        samples = sampler.run(np.asarray(u0, dtype=float), n_samples=n_samples, burn_in=burn_in,
+                              sample_interval=interval)
+    return samples, rec.decisions, rng.step + 1, inner.calls, inner.accepts
+
+
+# ------------------------------------------------------------ Lorenz-96
+def l96_ref_rhs(K, F):
+    """The reference RHS object: Lorenz96(K, J=0, F, h, c, b) (lorenz.py:13-111)."""
+    f = lorenz.Lorenz96(K, 0, F, 0.0, 0.0, 0.0)
+    return lambda x: f(0.0, x)
+
+
+def rk4_time_average(f, x0, dt, n):
+    """Classical RK4 + time average in the build's contract order (DESIGN.md §4,
+    REFERENCE arith), with the reference's RHS object as f."""
+    x = np.array(x0, dtype=np.float64)
+    h, h2, h6 = dt, dt * 0.5, dt / 6.0
+    ob = np.zeros_like(x)
+    for _ in range(n):
+        k1 = f(x)
+        k2 = f(x + h2 * k1)
+        k3 = f(x + h2 * k2)
+        k4 = f(x + h * k3)
+        x = x + h6 * (((k1 + 2.0 * k2) + 2.0 * k3) + k4)
+        ob = ob + x
+    return ob / float(n)
+
+
+def make_l96(out):
+    rng = np.random.default_rng(1234)
+    # RHS vectors: K=40 single scale, per-component forcing
+    X = rng.normal(0, 4, size=(64, 40))
+    F = 8.0 + rng.normal(0, 1, size=(64, 40))
+    R = np.stack([l96_ref_rhs(40, F[i])(X[i]) for i in range(64)])
+    # small-K cases incl. the edge K=4
+    X4 = rng.normal(0, 3, size=(16, 4))
+    F4 = rng.normal(8, 1, size=(16, 4))
+    R4 = np.stack([l96_ref_rhs(4, F4[i])(X4[i]) for i in range(16)])
+    # test_Lorenz96 known answers (lorenz.py:114-171), evaluated by the reference
+    kat = {
+        "forcing": (lorenz.Lorenz96(3, 1, 2, 1, 1, 1), [0, 0, 0, 0, 0, 0]),
+        "slow_nonlinearity": (lorenz.Lorenz96(4, 1, 0, 0, 0, 0), [1, 2, 3, 4, 0, 0, 0, 0]),
+        "fast_nonlinearity": (lorenz.Lorenz96(1, 4, 0, 0, 1, 2), [0, 1, 2, 3, 4]),
+        "step": (lorenz.Lorenz96(2, 2, 1, 1, 1, 1), [2, 3, 4, 5, 6, 7]),
+    }
+    for name, (obj, x) in kat.items():
+        out[f"l96_kat_{name}_in"] = np.asarray(x, dtype=float)
+        out[f"l96_kat_{name}_out"] = obj(1, np.asarray(x, dtype=float))
+    out["l96_rhs_x"], out["l96_rhs_F"], out["l96_rhs_out"] = X, F, R
+    out["l96_rhs4_x"], out["l96_rhs4_F"], out["l96_rhs4_out"] = X4, F4, R4
+
+    # Time-averaged RK4 forward map G with the reference RHS (K=40 and K=8)
+    for K, n, dt in ((40, 200, 0.005), (8, 300, 0.01)):
+        fm = np.full(K, 8.0)
+        x0 = 8.0 + rng.normal(0, 1, size=K)
+        U = rng.normal(0, 1, size=(6, K))
+        G = np.stack([rk4_time_average(l96_ref_rhs(K, fm + U[i]), x0, dt, n) for i in range(6)])
+        out[f"l96_G{K}_x0"], out[f"l96_G{K}_u"], out[f"l96_G{K}_G"] = x0, U, G
+        out[f"l96_G{K}_meta"] = np.array([n, dt])
+
+
+def make_l96_chain(out):
+    """pCN chains on Lorenz-96 K=8 through the reference sampler."""
+    K, n, dt = 8, 100, 0.01
+    rng = np.random.default_rng(99)
+    fm = np.full(K, 8.0)
+    x0 = 8.0 + rng.normal(0, 1, size=K)
+    utrue = 0.5 * rng.normal(size=K)
+    y = rk4_time_average(l96_ref_rhs(K, fm + utrue), x0, dt, n) + 0.05 * rng.normal(size=K)
+    gamma = 0.1
+    seed = 0x1234ABCD
+    chains = []
+    for chain in range(3):
+        def G(u):
+            return rk4_time_average(l96_ref_rhs(K, fm + u), x0, dt, n)
+
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, np.full(K, gamma**2), np.ones(K), 0.3, np.zeros(K), seed, chain, n_samples=6, burn_in=20,
+            interval=10)
+        chains.append((s, dec))
+    out["l96c_x0"], out["l96c_y"] = x0, y
+    out["l96c_meta"] = np.array([K, n, dt, gamma, 0.3, seed, 6, 20, 10], dtype=np.float64)
+    out["l96c_samples"] = np.stack([c[0] for c in chains])
+    out["l96c_decisions"] = np.stack([np.array(c[1]) for c in chains])
+
+
+# -------------------------------------------------------- linear Gaussian
+def make_linear(out):
+    """Config 1: G(u)=<g,u>, g=[3,1,4,1], u*=[2,7,1,8], γ=0.5,
+    prior N(0, I4), β=0.5, through the reference sampler with injected draws."""
+    g = np.array([3.0, 1.0, 4.0, 1.0])
+    ustar = np.array([2.0, 7.0, 1.0, 8.0])
+    gamma = 0.5
+    rng = np.random.default_rng(1)
+    y = np.array([np.dot(g, ustar) + gamma * rng.normal()])
+    seed = 20240501
+
+    def G(u):
+        return np.dot(g, u)  # stuart_examples.py:69-70
+
+    res = []
+    for chain in range(4):
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, np.array([gamma**2]), np.ones(4), 0.5, np.zeros(4), seed, chain, n_samples=40, burn_in=100,
+            interval=20)
+        res.append((s, dec, calls, accepts))
+    out["lin_g"], out["lin_y"] = g, y
+    out["lin_meta"] = np.array([gamma, 0.5, seed, 40, 100, 20], dtype=np.float64)
+    out["lin_samples"] = np.stack([r[0] for r in res])
+    out["lin_decisions"] = np.stack([np.array(r[1]) for r in res])
+    out["lin_counts"] = np.array([[r[2], r[3]] for r in res])
+    # EvolutionPotential values (potential.py:53-54) on random points: pins Φ up to its constant
+    U = np.random.default_rng(5).normal(size=(20, 4)) * 2
+    noise = GaussianDistribution(mean=np.zeros(1), covariance=np.array([[gamma**2]]))
+    pot = EvolutionPotential(G, y, noise)
+    out["lin_phi_u"] = U
+    out["lin_phi"] = np.array([pot(u) for u in U])
+
+
+# ---------------------------------------------------------------- Burgers
+def burgers_flux(w):
+    return 0.5 * w * w  # utilities.py:114-115 (BurgersEquation.flux)
+
+
+def burgers_flux_prime(w):
+    return w
+
+
+def ref_integrate(N, domain, theta, T):
+    """RusanovFVM.integrate (rusanov.py:31-60) of the reference, driven
+    step by step (its np.float line replaced by the same values computed here)."""
+    r = rusanov.RusanovFVM(burgers_flux, burgers_flux_prime, domain, N)
+    left, right, jump = 1 + theta[0], theta[1], theta[2]  # PerturbedRiemannIC, utilities.py:55-62
+    r.u[:] = np.array([left if x_ < jump else right for x_ in r.x], dtype=float)
+    t = 0
+    steps = 0
+    while t < T:  # rusanov.py:40-45
+        dt = r._cfl()
+        t += dt
+        r._step(dt)
+        steps += 1
+    return np.copy(r.u[1:-1]), t, steps, r.x, r.dx
+
+
+def make_burgers(out):
+    r = rusanov.RusanovFVM(burgers_flux, burgers_flux_prime, (0, 1), 10)
+    out["rus_kat_flux_in"] = np.array([[1, 1], [0, 1], [0, -1], [4, 5]], dtype=float)
+    out["rus_kat_flux_out"] = np.array([r._flux(a, b) for a, b in out["rus_kat_flux_in"]])
+    r3 = rusanov.RusanovFVM(burgers_flux, burgers_flux_prime, (0, 0.3), 3)
+    u = np.array([1, 1, -1, 2, 2], dtype=float)
+    r3._rate_of_change(u, 0.1)
+    out["rus_kat_rate_in"] = u
+    out["rus_kat_rate_dx"] = np.array([r3.dx])
+    out["rus_kat_rate_out"] = r3.dudt[1:-1].copy()
+    rng = np.random.default_rng(7)
+    wr = rng.normal(1, 1, size=66)
+    rr = rusanov.RusanovFVM(burgers_flux, burgers_flux_prime, (-1, 1), 64)
+    rr._rate_of_change(wr, 0.01)
+    out["rus_rate_w"], out["rus_rate_dx"], out["rus_rate_out"] = wr, np.array([rr.dx]), rr.dudt[1:-1].copy()
+
+    prior_mean = np.array([1.5, 0.25, -0.5])  # burgers_beta.py:64-67
+    points = np.array([-0.5, -0.25, 0.25, 0.5, 0.75])
+    interval = 0.1
+    for N in (32, 128, 256):
+        thetas = prior_mean + 0.25 * rng.normal(size=(4, 3))
+        thetas[0] = prior_mean
+        finals, ts, steps, meas = [], [], [], []
+        for th in thetas:
+            w, t, n, x, dx = ref_integrate(N, (-1, 1), th, 1.0)
+            xv = x[1:-1]
+            lo = np.searchsorted(xv, points - interval / 2, side="left")
+            hi = np.searchsorted(xv, points + interval / 2, side="left")
+            mdx = xv[1] - xv[0]
+            m = np.array([10 * np.trapz(w[a:b], dx=mdx) for a, b in zip(lo, hi)])  # utilities.py:100-109
+            finals.append(w)
+            ts.append(t)
+            steps.append(n)
+            meas.append(m)
+        out[f"bur{N}_theta"] = thetas
+        out[f"bur{N}_final"] = np.stack(finals)
+        out[f"bur{N}_t"] = np.array(ts)
+        out[f"bur{N}_steps"] = np.array(steps)
+        out[f"bur{N}_G"] = np.stack(meas)
+        out[f"bur{N}_x"], out[f"bur{N}_dx"] = x, np.array([dx])
+        out[f"bur{N}_win"] = np.stack([lo, hi])
+
+
+# ----------------------------------------------- distributions & schedule
+def make_misc(out):
+    g = GaussianDistribution(mean=np.array([1.0, -2.0, 0.5]), covariance=np.diag([0.5, 2.0, 1.5]))
+    X = np.random.default_rng(3).normal(size=(10, 3)) * 2
+    out["gauss_x"] = X
+    out["gauss_logpdf"] = np.array([g.logpdf(x) for x in X])
+    gf = GaussianDistribution(mean=np.array([0.0, 1.0]), covariance=np.array([[2.0, 0.5], [0.5, 1.0]]))
+    out["gaussfull_x"] = X[:, :2]
+    out["gaussfull_logpdf"] = np.array([gf.logpdf(x) for x in X[:, :2]])
+    # step-count arithmetic of MCMCSampler.run (sampler.py:18-26)
+    from ip_mcmc.test_utilities import MockProposer, MockRNG
+    from ip_mcmc import AnalyticAccepter
+    import contextlib
+    import io
+
+    rows = []
+    for b, n, s in ((100, 10, 20), (0, 5, 3), (50, 4, 50), (10, 3, 20), (1000, 2, 200)):
+        a = CountedAccepter(AnalyticAccepter(lambda x: x))
+        smp = MCMCSampler(MockProposer(), a, MockRNG(0.1))
+        with contextlib.redirect_stdout(io.StringIO()):
+            smp.run(np.array([1.0]), n_samples=n, burn_in=b, sample_interval=s)
+        rows.append([b, n, s, a.calls])
+    out["schedule"] = np.array(rows)
+
+
+def main():
+    out = {}
+    make_l96(out)
+    make_l96_chain(out)
+    make_linear(out)
+    make_burgers(out)
+    make_misc(out)
+    path = os.path.join(HERE, "reference_golden.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path)} bytes")
+
+
+if __name__ == "__main__":
+    main()

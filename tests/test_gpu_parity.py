@@ -1,0 +1,318 @@
+"""HIP kernels (libipmc.so, called through the C-ABI) vs the CPU oracle.
+
+Bar: bit-exact.  Every draw, every forward map, every Φ, every accept decision
+and every state must equal the oracle's on the same inputs, in fp32 and fp64
+and in both arithmetic modes.  The oracle itself is pinned to
+the reference in test_oracle_golden.py.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return torch.device("cuda", 0)
+
+
+def _t(a, dtype, dev):
+    return torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
+
+
+def _np(dtype):
+    return np.float32 if dtype == torch.float32 else np.float64
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+# ------------------------------------------------------------------- RNG
+def test_normals_bit_exact(dev, orc):
+    from ip_mcmc_amd import device as D
+
+    for step in (0, 1, 12345, (1 << 33) + 7):
+        z = D.normals(99, 5, 3000, step, 7, torch.float64, dev).cpu().numpy()
+        assert np.array_equal(z, orc.normals(99, 5, 3000, step, 7))
+        z32 = D.normals(99, 5, 300, step, 7, torch.float32, dev).cpu().numpy()
+        assert np.array_equal(z32, orc.normals(99, 5, 300, step, 7).astype(np.float32))
+
+
+def test_uniforms_bit_exact(dev, orc):
+    from ip_mcmc_amd import device as D
+
+    for seed in (0, 1, 2**63 + 5):
+        r = D.uniforms(seed, 3, 50_000, 77, dev).cpu().numpy()
+        assert np.array_equal(r, orc.uniforms(seed, 3, 50_000, 77))
+
+
+# ---------------------------------------------------------- forward maps
+def _ops():
+    from ip_mcmc_amd import LinearOperator, Lorenz63Operator, Lorenz96Operator
+
+    rng = np.random.default_rng(3)
+    ops = []
+    for arith in ("fma", "reference"):
+        ops.append(("lin", LinearOperator(rng.normal(size=(3, 5)), rng.normal(size=5), arith=arith)))
+        ops.append(("l63", Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=300, arith=arith)))
+        for K in (8, 40):
+            ops.append((f"l96_{K}", Lorenz96Operator(K, 8.0, dt=0.005, n_steps=200, arith=arith)))
+    return ops
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_forward_and_potential_bit_exact(dev, orc, dtype):
+    rng = np.random.default_rng(11)
+    for name, op in _ops():
+        U = 0.3 * rng.normal(size=(257, op.k))
+        g = op.forward_device(_t(U, dtype, dev)).cpu().numpy()
+        go = orc.forward(op, U, _np(dtype))
+        assert np.array_equal(g, go), (name, op.arith, np.abs(g - go).max())
+        y = go[0] + 0.1 * rng.normal(size=op.q)
+        ginv = 1.0 / (0.1 + rng.random(op.q))
+        from ip_mcmc_amd import EvolutionPotential, GaussianDistribution
+
+        pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(op.q), np.diag(1 / ginv**2)))
+        phi = pot.phi_device(_t(U, dtype, dev)).cpu().numpy()
+        phio = orc.potential(op, U, y, pot.device_terms()[1], _np(dtype))
+        assert np.array_equal(phi, phio), (name, op.arith)
+
+
+# ----------------------------------------------------------------- sweep
+def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, dev, lanes=0, box=None,
+                  sched=None, chain_offset=0, want_sums=False):
+    from ip_mcmc_amd import _abi
+    from ip_mcmc_amd._lib import call
+
+    U = _t(U0, dtype, dev)
+    phi = _t(phi0, dtype, dev)
+    acc = torch.zeros(U.shape[0], dtype=torch.int64, device=dev)
+    calls = torch.zeros(U.shape[0], dtype=torch.int64, device=dev)
+    yt, gt, st = _t(y, dtype, dev), _t(ginv, dtype, dev), _t(sq, dtype, dev)
+    m, _ = op.model(dtype, dev)
+    s = _abi.IpmcSweep()
+    s.dtype = _abi.F64 if dtype == torch.float64 else _abi.F32
+    s.lanes_per_chain = lanes
+    s.n_chains, s.chain_offset = U.shape[0], chain_offset
+    s.u, s.phi, s.accepts, s.calls = U.data_ptr(), phi.data_ptr(), acc.data_ptr(), calls.data_ptr()
+    s.y, s.gamma_inv, s.prior_sqrt = yt.data_ptr(), gt.data_ptr(), st.data_ptr()
+    keep = []
+    if box is not None:
+        bt = [None if b is None else _t(b, dtype, dev) for b in box]
+        keep += bt
+        s.box_lo, s.box_hi, s.box_off = [None if b is None else b.data_ptr() for b in bt]
+    if sched is not None:
+        sc = torch.as_tensor(sched).to(dev)
+        keep.append(sc)
+        s.beta_schedule = sc.data_ptr()
+    s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
+    s.seed, s.step0, s.n_steps = seed, step0, n_steps
+    samp = torch.zeros_like(U)
+    s.sample_out, s.sample_stride = samp.data_ptr(), U.shape[1]
+    sums = None
+    if want_sums:
+        sums = (torch.zeros(U.shape, dtype=torch.float64, device=dev),
+                torch.zeros(U.shape, dtype=torch.float64, device=dev))
+        s.sum_u, s.sum_u2 = sums[0].data_ptr(), sums[1].data_ptr()
+    call("ipmc_pcn_sweep", C.byref(m), C.byref(s), _stream(dev))
+    torch.cuda.synchronize(dev)
+    out = dict(u=U.cpu().numpy(), phi=phi.cpu().numpy(), acc=acc.cpu().numpy(), calls=calls.cpu().numpy(),
+               samp=samp.cpu().numpy())
+    if sums:
+        out["sum_u"], out["sum_u2"] = sums[0].cpu().numpy(), sums[1].cpu().numpy()
+    return out
+
+
+def _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, box=None, sched=None,
+                  chain_offset=0, want_sums=False):
+    npd = _np(dtype)
+    U = np.ascontiguousarray(U0.astype(npd))
+    phi = np.ascontiguousarray(phi0.astype(npd))
+    acc = np.zeros(U.shape[0], dtype=np.int64)
+    calls = np.zeros(U.shape[0], dtype=np.int64)
+    sums = (np.zeros(U.shape), np.zeros(U.shape)) if want_sums else None
+    orc.pcn_sweep(op, U, phi, y, ginv, sq, beta, seed, step0, n_steps, accepts=acc, calls=calls,
+                  chain_offset=chain_offset, box=box or (None, None, None), beta_schedule=sched, sums=sums,
+                  n_threads=8)
+    out = dict(u=U, phi=phi, acc=acc, calls=calls)
+    if want_sums:
+        out["sum_u"], out["sum_u2"] = sums
+    return out
+
+
+def _problem(op, n_chains, dtype, orc, seed=0):
+    rng = np.random.default_rng(seed)
+    U0 = 0.2 * rng.normal(size=(n_chains, op.k))
+    g = orc.forward(op, 0.1 * rng.normal(size=(1, op.k)))[0]
+    y = g + 0.05 * rng.normal(size=op.q)
+    ginv = np.full(op.q, 1 / 0.05)
+    sq = 0.5 + rng.random(op.k)
+    phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
+    return U0.astype(_np(dtype)).astype(np.float64), phi0, y, ginv, sq
+
+
+def _assert_same(a, b, what):
+    for key in ("u", "phi", "acc", "calls"):
+        assert np.array_equal(a[key], b[key]), (what, key)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_sweep_small_models_bit_exact(dev, orc, dtype):
+    for name, op in _ops():
+        if not name.startswith(("lin", "l63")):
+            continue
+        U0, phi0, y, ginv, sq = _problem(op, 300, dtype, orc)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 1234, 10, 25, dtype, dev)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 1234, 10, 25, dtype)
+        _assert_same(d, o, (name, op.arith))
+        assert np.array_equal(d["samp"], o["u"])
+        assert 0 < o["acc"].sum() < 300 * 25
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("K,lanes", [(8, 1), (8, 2), (8, 4), (40, 1), (40, 2), (40, 4), (40, 8)])
+def test_sweep_l96_bit_exact_every_layout(dev, orc, dtype, K, lanes):
+    from ip_mcmc_amd import Lorenz96Operator
+
+    if dtype == torch.float64 and K // lanes > 20:
+        pytest.skip("no fp64 instantiation with more than 20 components per lane")
+    for arith in ("fma", "reference"):
+        op = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=60, arith=arith)
+        U0, phi0, y, ginv, sq = _problem(op, 130, dtype, orc, seed=K)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype, dev, lanes=lanes)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype)
+        _assert_same(d, o, (K, lanes, arith))
+        assert np.array_equal(d["samp"], o["u"])
+
+
+def test_sweep_box_schedule_sums_offset(dev, orc):
+    """ConstrainAccepter box, VarStep beta schedule, running sums, chain offset."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    dtype = torch.float64
+    op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=40)
+    U0, phi0, y, ginv, sq = _problem(op, 200, dtype, orc, seed=5)
+    box = (np.full(8, -0.6), np.full(8, 0.6), np.zeros(8))
+    n = 12
+    sched = np.stack([np.linspace(0.1, 0.5, n), np.sqrt(1 - np.linspace(0.1, 0.5, n) ** 2)], axis=1)
+    d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 9, 100, n, dtype, dev, lanes=2, box=box, sched=sched,
+                      chain_offset=1000, want_sums=True)
+    o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 9, 100, n, dtype, box=box, sched=sched,
+                      chain_offset=1000, want_sums=True)
+    _assert_same(d, o, "box")
+    assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
+    assert (o["calls"] < n).any(), "box never rejected: test is vacuous"
+
+
+def test_sweep_split_launches_and_shards_identical(dev, orc):
+    """One launch of n steps == two launches; chains [0,C) == shards [0,a) + [a,C)."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    dtype = torch.float32
+    op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=50)
+    U0, phi0, y, ginv, sq = _problem(op, 256, dtype, orc, seed=8)
+    full = _sweep_device(op, U0, phi0, y, ginv, sq, 0.2, 3, 0, 8, dtype, dev)
+    a = _sweep_device(op, U0, phi0, y, ginv, sq, 0.2, 3, 0, 5, dtype, dev)
+    b = _sweep_device(op, a["u"], a["phi"], y, ginv, sq, 0.2, 3, 5, 3, dtype, dev)
+    assert np.array_equal(full["u"], b["u"]) and np.array_equal(full["acc"], a["acc"] + b["acc"])
+    s1 = _sweep_device(op, U0[:100], phi0[:100], y, ginv, sq, 0.2, 3, 0, 8, dtype, dev, chain_offset=0)
+    s2 = _sweep_device(op, U0[100:], phi0[100:], y, ginv, sq, 0.2, 3, 0, 8, dtype, dev, chain_offset=100)
+    assert np.array_equal(full["u"], np.concatenate([s1["u"], s2["u"]]))
+
+
+def test_headline_shape_subset_bit_exact(dev, orc):
+    """Config 3 shape (d=40, 2000 RK4 steps, 65 536 chains, fp32 and fp64): one
+    pCN step of the whole ensemble on the device; 48 chains re-run on the oracle."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=2000)
+    C_ = 65536
+    rng = np.random.default_rng(21)
+    idx = np.sort(rng.choice(C_, 48, replace=False))
+    for dtype in (torch.float32, torch.float64):
+        U0, phi0, y, ginv, sq = _problem(op, C_, dtype, orc, seed=21)
+        d = _sweep_device(op, U0, phi0, y, ginv, np.ones(40), 0.2, 5, 0, 1, dtype, dev)
+        for i in idx:
+            o = _sweep_oracle(orc, op, U0[i:i + 1], phi0[i:i + 1], y, ginv, np.ones(40), 0.2, 5, 0, 1, dtype,
+                              chain_offset=int(i))
+            assert np.array_equal(d["u"][i], o["u"][0]) and d["acc"][i] == o["acc"][0], (dtype, i)
+        assert np.all(np.isfinite(d["phi"]))
+
+
+# ------------------------------------------------------------- sampler API
+def test_sampler_linear_gaussian_posterior(dev):
+    """Config 1 problem (stuart_examples.py-style linear G) through MCMCSampler:
+    the posterior mean over 4096 chains matches the analytic Gaussian posterior
+    (results.org:59-62) within 4 Monte-Carlo standard errors."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             LinearOperator, MCMCSampler, pCNAccepter)
+
+    g = np.array([3.0, 1.0, 4.0, 1.0])
+    gamma, y = 0.5, np.array([np.dot(g, [2.0, 7.0, 1.0, 8.0]) + 0.3])
+    prior = GaussianDistribution(np.zeros(4), np.eye(4))
+    pot = EvolutionPotential(LinearOperator(g), y, GaussianDistribution(0, gamma**2))
+    acc = CountedAccepter(pCNAccepter(pot))
+    s = MCMCSampler(ConstSteppCNProposer(0.5, prior), acc, 7)
+    C_ = 4096
+    samples = s.run(np.zeros((C_, 4)), n_samples=50, burn_in=200, sample_interval=10)
+    assert samples.shape == (C_, 50, 4)
+    S0g = g
+    denom = gamma**2 + g @ g
+    m = S0g * y[0] / denom
+    cov = np.eye(4) - np.outer(S0g, S0g) / denom
+    est = samples[:, -1, :].mean(axis=0)
+    se = np.sqrt(np.diag(cov) / C_)
+    assert np.all(np.abs(est - m) < 4 * se + 1e-3), (est, m)
+    r = acc.ratio()
+    assert r.shape == (C_,) and 0.2 < r.mean() < 0.95
+    assert int(acc.calls[0]) == max(0, 200 - 10) + 50 * 10
+
+
+def test_sampler_single_chain_matches_reference_fixture(dev, golden):
+    """The drop-in path: one chain, reference API, reference fixture (linear,
+    injected draws) reproduced by MCMCSampler on the GPU."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             LinearOperator, MCMCSampler, PhiloxRNG, pCNAccepter)
+
+    gamma, beta, seed, n_samples, burn_in, interval = golden["lin_meta"]
+    pot = EvolutionPotential(LinearOperator(golden["lin_g"], arith="reference"), golden["lin_y"],
+                             GaussianDistribution(0, gamma**2))
+    for chain in range(4):
+        acc = CountedAccepter(pCNAccepter(pot))
+        s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))), acc,
+                        PhiloxRNG(int(seed)), chain_offset=chain)
+        out = s.run(np.zeros(4), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+        assert out.shape == (int(n_samples), 4)
+        assert np.array_equal(out, golden["lin_samples"][chain])
+        assert acc.accepts == int(golden["lin_counts"][chain, 1])
+        assert acc.calls == int(golden["lin_counts"][chain, 0])
+
+
+def test_sampler_l96_chain_matches_reference_fixture(dev, golden):
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, Lorenz96Operator,
+                             MCMCSampler, PhiloxRNG, pCNAccepter)
+
+    K, n, dt, gamma, beta, seed, n_samples, burn_in, interval = golden["l96c_meta"]
+    K = int(K)
+    op = Lorenz96Operator(K, 8.0, x0=golden["l96c_x0"], dt=dt, n_steps=int(n), arith="reference")
+    pot = EvolutionPotential(op, golden["l96c_y"], GaussianDistribution(np.zeros(K), gamma**2 * np.eye(K)))
+    s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(K), np.eye(K))), pCNAccepter(pot),
+                    PhiloxRNG(int(seed)))
+    out = s.run(np.zeros((3, K)), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+    assert np.array_equal(out, golden["l96c_samples"])
+
+
+def test_sampler_rejects_host_callables(dev):
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, MCMCSampler,
+                             UnsupportedOnDevice, pCNAccepter)
+
+    pot = EvolutionPotential(lambda u: u, np.zeros(2), GaussianDistribution(np.zeros(2), np.eye(2)))
+    s = MCMCSampler(ConstSteppCNProposer(0.5, GaussianDistribution(np.zeros(2), np.eye(2))), pCNAccepter(pot), 1)
+    with pytest.raises(UnsupportedOnDevice):
+        s.run(np.zeros(2), 2, 0, 1)

@@ -1,0 +1,152 @@
+"""The CPU oracle (oracle/liboracle.so) pinned against the reference.
+
+Fixtures: tests/golden/reference_golden.npz, made by tests/golden/make_golden.py
+from the reference itself (ochsnerd/ip_mcmc in /root/reference).
+"""
+import numpy as np
+import pytest
+
+from ip_mcmc_amd.forward import BurgersOperator, LinearOperator, Lorenz96Operator
+
+
+# ----------------------------------------------------------------- RNG
+def test_philox_random123_kats(orc):
+    # Random123 known-answer vectors for philox4x32-10
+    assert list(orc.philox([0, 0, 0, 0], [0, 0])) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert list(orc.philox([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2)) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert list(orc.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0])) == [
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_det_log_accuracy(orc):
+    x = np.exp(np.random.default_rng(0).uniform(-37.0, 0.0, 200_000))
+    x = np.concatenate([x, [1.0, 2.0**-53, 0.5, np.nextafter(1.0, 0.0)]])
+    err = np.abs(orc.det_log(x) - np.log(x))
+    assert err.max() < 4e-15
+    assert orc.det_log(np.array([0.0]))[0] == -np.inf
+
+
+def test_det_sincos_accuracy(orc):
+    t = np.concatenate([np.random.default_rng(1).random(200_000), [0.0, 0.125, 0.25, 0.5, 0.75, 1 - 2.0**-53]])
+    s, c = orc.sincos_2pi(t)
+    assert np.abs(s - np.sin(2 * np.pi * t)).max() < 2e-15
+    assert np.abs(c - np.cos(2 * np.pi * t)).max() < 2e-15
+    assert np.all(s * s + c * c <= 1 + 4e-16)
+
+
+def test_normals_and_uniforms_distribution(orc):
+    z = orc.normals(7, 0, 100_000, 3, 4).ravel()
+    assert abs(z.mean()) < 0.01 and abs(z.var() - 1) < 0.01
+    assert abs((z**4).mean() - 3) < 0.05
+    r = orc.uniforms(7, 0, 100_000, 3)
+    assert r.min() >= 0 and r.max() < 1 and abs(r.mean() - 0.5) < 0.005
+    # counter-based: a chain's draw depends on its global id only
+    a = orc.normals(7, 10, 5, 3, 4)
+    b = orc.normals(7, 0, 20, 3, 4)[10:15]
+    assert np.array_equal(a, b)
+
+
+# ------------------------------------------------------------ Lorenz-96
+def test_l96_rhs_reference_order_bit_exact(orc, golden):
+    """REFERENCE arith reproduces Lorenz96.__call__ (lorenz.py:77-81) bit for bit."""
+    for pre in ("l96_rhs", "l96_rhs4"):
+        X, F, R = golden[pre + "_x"], golden[pre + "_F"], golden[pre + "_out"]
+        got = np.stack([orc.l96_rhs(X[i], F[i], "reference") for i in range(len(X))])
+        assert np.array_equal(got, R)
+
+
+def test_l96_rhs_fma_close(orc, golden):
+    X, F, R = golden["l96_rhs_x"], golden["l96_rhs_F"], golden["l96_rhs_out"]
+    got = np.stack([orc.l96_rhs(X[i], F[i], "fma") for i in range(len(X))])
+    np.testing.assert_allclose(got, R, rtol=0, atol=1e-13 * np.abs(X).max() ** 2)
+
+
+@pytest.mark.parametrize("name,K,F", [("forcing", 3, 2.0), ("slow_nonlinearity", 4, 0.0)])
+def test_l96_reference_kats(orc, golden, name, K, F):
+    """lorenz.py:114-171 known answers (slow part; the build's L96 is single scale)."""
+    x = golden[f"l96_kat_{name}_in"][:K]
+    want = golden[f"l96_kat_{name}_out"][:K]
+    assert np.array_equal(orc.l96_rhs(x, F, "reference"), want)
+
+
+@pytest.mark.parametrize("K", [40, 8])
+def test_l96_forward_reference_bit_exact(orc, golden, K):
+    """G(u) (RK4 time average) with the reference RHS object vs the oracle, fp64."""
+    n, dt = golden[f"l96_G{K}_meta"]
+    op = Lorenz96Operator(K, 8.0, x0=golden[f"l96_G{K}_x0"], dt=dt, n_steps=int(n), arith="reference")
+    got = orc.forward(op, golden[f"l96_G{K}_u"])
+    assert np.array_equal(got, golden[f"l96_G{K}_G"])
+    op_f = Lorenz96Operator(K, 8.0, x0=golden[f"l96_G{K}_x0"], dt=dt, n_steps=int(n), arith="fma")
+    np.testing.assert_allclose(orc.forward(op_f, golden[f"l96_G{K}_u"]), golden[f"l96_G{K}_G"], rtol=1e-9)
+
+
+def _replay(orc, op, meta_samples, y, gamma, beta, seed, n_samples, burn_in, interval, n_chains, prior_sqrt):
+    U = np.zeros((n_chains, op.k))
+    ginv = np.full(op.q, 1.0 / gamma)
+    phi = orc.potential(op, U, y, ginv)
+    acc = np.zeros(n_chains, dtype=np.int64)
+    step = 0
+    nb = max(0, burn_in - interval)
+    orc.pcn_sweep(op, U, phi, y, ginv, prior_sqrt, beta, seed, step, nb, accepts=acc)
+    step += nb
+    samples = np.zeros((n_chains, n_samples, op.k))
+    for i in range(n_samples):
+        orc.pcn_sweep(op, U, phi, y, ginv, prior_sqrt, beta, seed, step, interval, accepts=acc)
+        step += interval
+        samples[:, i] = U
+    return samples, acc
+
+
+def test_linear_chain_matches_reference_sampler(orc, golden):
+    """Config 1 through the reference MCMCSampler (injected draws) vs the oracle."""
+    gamma, beta, seed, n_samples, burn_in, interval = golden["lin_meta"]
+    op = LinearOperator(golden["lin_g"], arith="reference")
+    samples, acc = _replay(orc, op, None, golden["lin_y"], gamma, beta, int(seed), int(n_samples), int(burn_in),
+                           int(interval), 4, np.ones(4))
+    assert np.array_equal(acc, golden["lin_decisions"].sum(axis=1))
+    assert np.array_equal(acc, golden["lin_counts"][:, 1])
+    np.testing.assert_array_equal(samples, golden["lin_samples"])
+
+
+def test_linear_potential_matches_reference_up_to_constant(orc, golden):
+    gamma = golden["lin_meta"][0]
+    op = LinearOperator(golden["lin_g"], arith="reference")
+    phi = orc.potential(op, golden["lin_phi_u"], golden["lin_y"], [1 / gamma])
+    const = 0.5 * (np.log(2 * np.pi) + np.log(gamma**2))
+    np.testing.assert_allclose(phi + const, golden["lin_phi"], rtol=1e-13, atol=1e-12)
+
+
+def test_l96_chain_matches_reference_sampler(orc, golden):
+    K, n, dt, gamma, beta, seed, n_samples, burn_in, interval = golden["l96c_meta"]
+    K = int(K)
+    op = Lorenz96Operator(K, 8.0, x0=golden["l96c_x0"], dt=dt, n_steps=int(n), arith="reference")
+    samples, acc = _replay(orc, op, None, golden["l96c_y"], gamma, beta, int(seed), int(n_samples), int(burn_in),
+                           int(interval), 3, np.ones(K))
+    assert np.array_equal(acc, golden["l96c_decisions"].sum(axis=1))
+    np.testing.assert_array_equal(samples, golden["l96c_samples"])
+
+
+# ---------------------------------------------------------------- Burgers
+def test_rusanov_kats(orc, golden):
+    """rusanov.py:144-164 known answers, evaluated by the reference."""
+    for (a, b), want in zip(golden["rus_kat_flux_in"], golden["rus_kat_flux_out"]):
+        assert orc.rusanov_flux(a, b) == want
+    r = orc.rusanov_rate(golden["rus_kat_rate_in"], golden["rus_kat_rate_dx"][0])
+    assert np.array_equal(r[1:-1], golden["rus_kat_rate_out"])
+    np.testing.assert_allclose(r[1:-1], [-10, 32.5, -37.5])
+    r = orc.rusanov_rate(golden["rus_rate_w"], golden["rus_rate_dx"][0])
+    assert np.array_equal(r[1:-1], golden["rus_rate_out"])
+
+
+@pytest.mark.parametrize("N", [32, 128, 256])
+def test_burgers_forward_reference_bit_exact(orc, golden, N):
+    """FVMObservationOperator = Measurer(RusanovFVM.integrate(IC)) of the reference vs the oracle, fp64, CFL dt."""
+    op = BurgersOperator(prior_mean=(0.0, 0.0, 0.0), N=N, T=1.0, dt_mode="cfl", arith="reference")
+    np.testing.assert_array_equal(op.x, golden[f"bur{N}_x"])
+    assert op.dx == golden[f"bur{N}_dx"][0]
+    np.testing.assert_array_equal(np.stack([op.win_lo, op.win_hi]), golden[f"bur{N}_win"])
+    G = orc.forward(op, golden[f"bur{N}_theta"])
+    np.testing.assert_array_equal(G, golden[f"bur{N}_G"])
+    op_f = BurgersOperator(prior_mean=(0.0, 0.0, 0.0), N=N, T=1.0, dt_mode="cfl", arith="fma")
+    np.testing.assert_allclose(orc.forward(op_f, golden[f"bur{N}_theta"]), golden[f"bur{N}_G"], rtol=1e-9,
+                               atol=1e-12)
