@@ -86,6 +86,10 @@ def call_auto(model, adt, n):
     return lib().ipmc_auto_lanes(C.byref(model), adt, n)
 
 
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def barrier(world):
     if world > 1:
         dist.barrier()
@@ -124,18 +128,20 @@ def cpu_baseline(op, y, dtype_np, budget_s=15.0):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
 
+    ginv = np.full(D, 1 / GAMMA)
+    phi0 = O.potential(op, np.zeros((1, D), dtype=dtype_np), y, ginv, dtype_np)[0]
+
     def run(nc):
-        U = np.zeros((nc, D), dtype=dtype_np)
-        ginv = np.full(D, 1 / GAMMA)
-        phi = O.potential(op, U, y, ginv, dtype_np)
+        U = np.zeros((nc, D), dtype=dtype_np)  # every chain starts at u = 0, as on the GPU
+        phi = np.full(nc, phi0, dtype=dtype_np)
         acc = np.zeros(nc, dtype=np.int64)
         t0 = time.perf_counter()
         O.pcn_sweep(op, U, phi, y, ginv, np.ones(D), BETA, 2, 0, 1, accepts=acc, n_threads=threads)
         return time.perf_counter() - t0
 
     t1 = run(threads)  # one chain-step per thread, calibration
-    per = t1 / threads
-    n = int(max(threads, min(1_000_000, budget_s / max(per, 1e-6) * threads * 0.8)))
+    per = t1 / threads  # wall seconds per chain-step with all threads busy
+    n = int(max(threads, min(1_000_000, budget_s / max(per, 1e-9))))
     n = (n // threads) * threads
     el = run(n)
     return {"value": n / el, "unit": "pCN steps/s", "cores": threads, "kind": "port",
@@ -163,10 +169,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    log(f"rank {rank}/{world} on {dev}: building the problem")
     op, y = problem()
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     w = Workload(op, y, args.chains, rank * args.chains, tdt, dev, args.lanes)
+    log(f"timing {args.steps} sweeps ({args.dtype}, {args.chains} chains/GPU, lanes={w.lanes})")
     el, kern_ms = timed(w, args.steps, args.warmup, world)
+    log(f"{args.dtype}: {el:.3f} s, kernel {kern_ms:.3f} ms/launch")
     total_steps = world * args.chains * args.steps
     value = total_steps / el
 
@@ -182,6 +191,7 @@ def main():
         other = torch.float32 if tdt == torch.float64 else torch.float64
         w2 = Workload(op, y, args.chains, rank * args.chains, other, dev, args.lanes)
         el2, k2 = timed(w2, args.steps, args.warmup, world)
+        log(f"{other}: kernel {k2:.3f} ms/launch")
         key = "f32" if other == torch.float32 else "f64"
         extra[f"{key}_pcn_steps_per_s"] = world * args.chains * args.steps / el2
         extra[f"{key}_kernel_ms"] = k2
@@ -194,6 +204,7 @@ def main():
     hbm_bytes = args.chains * D * (2 if tdt == torch.float32 else 4) * 2 * 2  # u read+write, sq/y/.. via cache
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
+        log("CPU baseline (C oracle)")
         cpu = cpu_baseline(op, y, np.float64 if tdt == torch.float64 else np.float32)
 
     if rank == 0:

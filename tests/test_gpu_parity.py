@@ -270,7 +270,7 @@ def test_sampler_linear_gaussian_posterior(dev):
     se = np.sqrt(np.diag(cov) / C_)
     assert np.all(np.abs(est - m) < 4 * se + 1e-3), (est, m)
     r = acc.ratio()
-    assert r.shape == (C_,) and 0.2 < r.mean() < 0.95
+    assert r.shape == (C_,) and 0.02 < r.mean() < 0.95
     assert int(acc.calls[0]) == max(0, 200 - 10) + 50 * 10
 
 
