@@ -1,16 +1,429 @@
-// Burgers (Rusanov FV + SSPRK2) kernels — placeholder until the wave-cooperative kernel lands.
+// Burgers forward map (Rusanov FV + SSPRK2, burgers/rusanov.py:6-109) and its
+// pCN sweep.
+//
+// Layout: one chain per group of GS lanes (GS in {16, 32, 64}, groups aligned
+// inside a wavefront); lane `sub` owns CPL consecutive interior cells
+// [sub*CPL + 1, sub*CPL + CPL] in VGPRs (N = nlive*CPL, nlive <= GS; lanes past
+// nlive hold no cells).  The ghost cells are explicit values on the first and
+// last live lane (the IC sets them, rusanov.py:32, and the first step reads
+// them before any boundary condition is applied).  Interface fluxes between
+// lanes use the neighbour lane's edge cell (ds_bpermute); each lane computes
+// CPL+1 fluxes, the shared edge flux bit-identically on both sides.  CFL mode
+// reduces max|w| over the group every step (exact, order-free); fixed-dt mode
+// keeps a per-lane guard and reduces once.  The final interior state is staged
+// in LDS and lane 0 of the group evaluates the Measurer windows in numpy's
+// pairwise summation order (so REFERENCE arith equals np.trapz bit for bit).
 #include "ipmc_internal.hpp"
+#include "ipmc_sweep_common.hpp"
 
 namespace ipmc {
 
-int burgers_sweep(const ipmc_model&, const ipmc_sweep&, hipStream_t) {
-  set_error("Burgers sweep: not built yet");
+constexpr int kBurBlock = 256;
+
+template <typename T, bool FM>
+__device__ __forceinline__ T rus_flux(T a, T b) {
+  const T half = (T)0.5;
+  const T aa = a < (T)0 ? -a : a, ab = b < (T)0 ? -b : b;
+  const T sp = ab > aa ? ab : aa;
+  if constexpr (FM) {
+    const T fb = (half * b) * b;
+    const T favg = half * madd<true>(half * a, a, fb);
+    return madd<true>(-(half * sp), b - a, favg);
+  } else {
+    const T fa = (half * a) * a, fb = (half * b) * b;
+    const T favg = half * (fa + fb);
+    return favg - (half * sp) * (b - a);
+  }
+}
+
+template <int GS, typename T>
+__device__ __forceinline__ T group_max_abs(T m) {
+#pragma unroll
+  for (int off = GS / 2; off >= 1; off >>= 1) {
+    const T o = __shfl_xor(m, off, 64);
+    m = (o > m) ? o : m;
+  }
+  return m;
+}
+
+template <int CPL, typename T>
+__device__ __forceinline__ T lane_max_abs(const T (&w)[CPL], bool live) {
+  T m = (T)0;
+  if (live) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const T a = w[j] < (T)0 ? -w[j] : w[j];
+      if (a > m) m = a;
+    }
+  }
+  return m;
+}
+
+// dudt for the lane's cells from state s (+ halos hl / hr).
+template <typename T, int CPL, bool FM>
+__device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, T mdx, T nudx2, bool visc, T (&r)[CPL]) {
+  T fl = rus_flux<T, FM>(hl, s[0]);
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const T right = (j + 1 < CPL) ? s[j + 1] : hr;
+    const T left = (j > 0) ? s[j - 1] : hl;
+    const T fr = rus_flux<T, FM>(s[j], right);
+    T v = (fr - fl) / mdx;
+    if (visc) {
+      const T lap = (right - (s[j] + s[j])) + left;
+      v = madd<FM>(nudx2, lap, v);
+    }
+    r[j] = v;
+    fl = fr;
+  }
+}
+
+struct BurCtx {
+  int sub, lane, nlive;
+};
+
+// Halo exchange inside the group: value of the previous lane's last cell and
+// the next lane's first cell (or the ghosts at the ends).
+template <typename T, int CPL>
+__device__ __forceinline__ void halos(const T (&s)[CPL], T gl, T gr, const BurCtx& c, T& hl, T& hr) {
+  hl = __shfl(s[CPL - 1], c.lane - 1, 64);
+  hr = __shfl(s[0], c.lane + 1, 64);
+  if (c.sub == 0) hl = gl;
+  if (c.sub == c.nlive - 1) hr = gr;
+}
+
+// Integrate the Riemann IC (left, right, jump) to the end; returns validity.
+// w holds the final interior cells of this lane.
+template <typename T, int CPL, int GS, bool FM>
+__device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, const BurCtx& c, T (&w)[CPL]) {
+  const bool live = c.sub < c.nlive;
+  const T* xc = (const T*)m.x0;
+  const int c0 = c.sub * CPL + 1;  // first owned cell (ghost-inclusive index)
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int idx = live ? c0 + j : 1;
+    w[j] = (xc[idx] < jump) ? left : right;
+  }
+  const int N = m.dim;
+  T gl = (xc[0] < jump) ? left : right;
+  T gr = (xc[N + 1] < jump) ? left : right;
+  const T dx = (T)m.dx, mdx = -dx;
+  const T cfl_dx = (T)m.cfl * dx;
+  const bool visc = (m.nu != 0.0);
+  const T nudx2 = (T)m.nu / (dx * dx);
+  const T tend = (T)m.t_end;
+  const T dtf = (T)m.dt;
+  const bool cflmode = (m.dt_mode == IPMC_DT_CFL);
+  bool valid = true;
+  bool lane_ok = true;
+  T t = (T)0;
+  int iters = 0;
+  for (;;) {
+    T dt;
+    if (cflmode) {
+      const T mx = group_max_abs<GS>(lane_max_abs<CPL>(w, live));
+      if (!(t < tend)) break;
+      if (iters >= m.max_iter) {
+        valid = false;
+        break;
+      }
+      dt = cfl_dx / mx;
+      t = t + dt;
+    } else {
+      if (iters >= m.n_steps) break;
+      const T mx = lane_max_abs<CPL>(w, live);
+      if (!(mx * dtf <= cfl_dx)) lane_ok = false;
+      dt = dtf;
+    }
+    ++iters;
+    // SSPRK2, rusanov.py:62-74
+    T hl, hr, r[CPL], ws[CPL];
+    halos<T, CPL>(w, gl, gr, c, hl, hr);
+    rus_rate<T, CPL, FM>(w, hl, hr, mdx, nudx2, visc, r);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) ws[j] = madd<FM>(dt, r[j], w[j]);
+    const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
+    halos<T, CPL>(ws, gls, grs, c, hl, hr);
+    rus_rate<T, CPL, FM>(ws, hl, hr, mdx, nudx2, visc, r);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      ws[j] = madd<FM>(dt, r[j], ws[j]);
+      w[j] = (w[j] + ws[j]) / (T)2;
+    }
+    gl = w[0];
+    gr = w[CPL - 1];
+  }
+  if (!cflmode) {
+    // the group is valid iff every live lane kept max|w| dt <= cfl dx
+    const unsigned long long bad = __ballot(!lane_ok);
+    const unsigned long long gmask = (GS == 64 ? ~0ull : ((1ull << GS) - 1)) << (c.lane & ~(GS - 1));
+    valid = (bad & gmask) == 0;
+  }
+  return valid;
+}
+
+// numpy pairwise sum (loops_utils.h.src, n <= 128) of the trapz terms
+// (mdx * (v[i+1] + v[i])) / 2, i = 0..n-1, with v in LDS.
+template <typename T>
+__device__ T trapz_pairwise(const T* v, int n, T mdx) {
+  auto term = [&](int i) { return (mdx * (v[i + 1] + v[i])) / (T)2.0; };
+  if (n < 8) {
+    T res = (T)0;
+    for (int i = 0; i < n; ++i) res = res + term(i);
+    return res;
+  }
+  T r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = term(j);
+  int i;
+  for (i = 8; i < n - (n % 8); i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + term(i + j);
+  }
+  T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res = res + term(i);
+  return res;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// G(theta) for the chain, state staged through `row` (this chain's N
+// interior cells in LDS).  Lane 0 of the group evaluates the windows and,
+// for PHI, the misfit; g_out (if set) receives G.  Returns Φ (+inf if the
+// integration was invalid) on lane 0 of the group.
+template <typename T, int CPL, int GS, bool FM>
+__device__ T burgers_phi(const ipmc_model& m, const T (&v)[3], const BurCtx& c, T* row, const T* y, const T* ginv,
+                         T* g_out) {
+  const T* th0 = (const T*)m.theta0;
+  const T left = (T)1 + (th0[0] + v[0]);
+  const T right = th0[1] + v[1];
+  const T jump = th0[2] + v[2];
+  T w[CPL];
+  const bool valid = burgers_integrate<T, CPL, GS, FM>(m, left, right, jump, c, w);
+  if (c.sub < c.nlive) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) row[c.sub * CPL + j] = w[j];
+  }
+  wave_sync_lds();
+  T phi = (T)0;
+  if (c.sub == 0) {
+    const T mdxm = (T)m.meas_dx;
+    T acc = (T)0;
+    for (int j = 0; j < m.q; ++j) {
+      T gj = (T)__builtin_nan("");
+      if (valid) {
+        const int lo = m.win_lo[j], hi = m.win_hi[j];
+        int nt = hi - lo - 1;
+        if (nt < 0) nt = 0;
+        gj = (T)m.meas_scale * trapz_pairwise<T>(row + lo, nt, mdxm);
+      }
+      if (g_out) g_out[j] = gj;
+      if (y) {
+        const T r = (y[j] - gj) * ginv[j];
+        acc = madd<FM>(r, r, acc);
+      }
+    }
+    phi = valid ? (T)0.5 * acc : (T)__builtin_inf();
+  }
+  wave_sync_lds();  // row is reused by the next evaluation
+  return phi;
+}
+
+constexpr int kBurQMax = 64;
+
+template <typename T, int CPL, int GS, bool FM>
+__global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
+  __shared__ T lds[kBurBlock * CPL];
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * kBurBlock + threadIdx.x;
+  const int64_t chain = tid / GS;
+  const BurCtx c{(int)(tid % GS), lane, m.dim / CPL};
+  if (chain >= s.n_chains) return;
+  T* row = lds + (threadIdx.x & ~(GS - 1)) * CPL;
+  const uint64_t gid = (uint64_t)(s.chain_offset + chain);
+  T* u = (T*)s.u + chain * 3;
+  T ur[3] = {u[0], u[1], u[2]};  // every lane of the group keeps the chain state
+  const T* sq = (const T*)s.prior_sqrt;
+  const T beta = (T)s.beta, contr = (T)s.contraction;
+  T* phi = (T*)s.phi;
+  T phu = phi[chain];
+  int64_t nacc = 0, ncalls = 0;
+  for (int64_t st = 0; st < s.n_steps; ++st) {
+    const uint64_t step = s.step0 + (uint64_t)st;
+    const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
+    const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
+    T v[3];
+    pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v);
+    bool ok = true;
+    if (s.box_lo || s.box_hi) {
+      const T* lo = (const T*)s.box_lo;
+      const T* hi = (const T*)s.box_hi;
+      const T* off = (const T*)s.box_off;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const T t = v[j] + (off ? off[j] : (T)0);
+        if (lo && !(lo[j] < t)) ok = false;
+        if (hi && !(t < hi[j])) ok = false;
+      }
+    }
+    if (ok) {
+      ++ncalls;
+      T phv = burgers_phi<T, CPL, GS, FM>(m, v, c, row, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
+      phv = __shfl(phv, lane & ~(GS - 1), 64);
+      if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) ur[j] = v[j];
+        phu = phv;
+        ++nacc;
+      }
+    }
+    if (s.sum_u && c.sub == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double ud = (double)ur[j];
+        s.sum_u[chain * 3 + j] += ud;
+        if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+      }
+    }
+  }
+  if (c.sub == 0) {
+    phi[chain] = phu;
+    if (s.accepts) s.accepts[chain] += nacc;
+    if (s.calls) s.calls[chain] += ncalls;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) u[j] = ur[j];
+    if (s.sample_out) {
+      T* so = (T*)s.sample_out + chain * s.sample_stride;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) so[j] = ur[j];
+    }
+  }
+}
+
+template <typename T, int CPL, int GS, bool FM, bool PHI>
+__global__ __launch_bounds__(kBurBlock) void burgers_eval_kernel(const ipmc_model m, int64_t n,
+                                                                 const T* __restrict__ uin, const T* __restrict__ y,
+                                                                 const T* __restrict__ ginv, T* __restrict__ out) {
+  __shared__ T lds[kBurBlock * CPL];
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * kBurBlock + threadIdx.x;
+  const int64_t chain = tid / GS;
+  const BurCtx c{(int)(tid % GS), lane, m.dim / CPL};
+  if (chain >= n) return;
+  T* row = lds + (threadIdx.x & ~(GS - 1)) * CPL;
+  const T v[3] = {uin[chain * 3], uin[chain * 3 + 1], uin[chain * 3 + 2]};
+  const T ph = burgers_phi<T, CPL, GS, FM>(m, v, c, row, PHI ? y : nullptr, ginv, PHI ? nullptr : out + chain * m.q);
+  if (PHI && c.sub == 0) out[chain] = ph;
+}
+
+// ------------------------------------------------------------------ host
+// Supported layouts: CPL cells per lane, GS lanes per chain.
+static bool pick(int N, int64_t n_chains, int& cpl, int& gs) {
+  // Prefer 8 cells per lane; fall back to 4 when a chain does not fill 8-cell lanes.
+  const int cands[2] = {8, 4};
+  for (int c : cands) {
+    if (N % c) continue;
+    const int need = N / c;
+    const int groups[3] = {16, 32, 64};
+    for (int g : groups) {
+      if (need <= g) {
+        cpl = c;
+        gs = g;
+        return true;
+      }
+    }
+  }
+  (void)n_chains;
+  return false;
+}
+
+template <typename T, int CPL, int GS, bool FM>
+static int launch_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  const int64_t blocks = (s.n_chains * GS + kBurBlock - 1) / kBurBlock;
+  hipLaunchKernelGGL((burgers_sweep_kernel<T, CPL, GS, FM>), dim3((unsigned)blocks), dim3(kBurBlock), 0, st, m, s);
+  return check_launch("burgers_sweep_kernel");
+}
+
+template <typename T, int CPL, int GS, bool FM>
+static int launch_eval(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
+                       bool phi, hipStream_t st) {
+  const int64_t blocks = (n * GS + kBurBlock - 1) / kBurBlock;
+  if (phi)
+    hipLaunchKernelGGL((burgers_eval_kernel<T, CPL, GS, FM, true>), dim3((unsigned)blocks), dim3(kBurBlock), 0, st,
+                       m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);
+  else
+    hipLaunchKernelGGL((burgers_eval_kernel<T, CPL, GS, FM, false>), dim3((unsigned)blocks), dim3(kBurBlock), 0, st,
+                       m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);
+  return check_launch("burgers_eval_kernel");
+}
+
+template <typename T, bool FM, typename F>
+static int dispatch(int cpl, int gs, F&& f) {
+#define IPMC_BUR(C, G) \
+  if (cpl == C && gs == G) return f.template operator()<T, C, G, FM>();
+  IPMC_BUR(8, 16) IPMC_BUR(8, 32) IPMC_BUR(8, 64) IPMC_BUR(4, 16) IPMC_BUR(4, 32) IPMC_BUR(4, 64)
+#undef IPMC_BUR
   return IPMC_ERR_UNSUPPORTED;
 }
-int burgers_eval(const ipmc_model&, int32_t, int64_t, const void*, const void*, const void*, void*, bool,
-                 hipStream_t) {
-  set_error("Burgers eval: not built yet");
-  return IPMC_ERR_UNSUPPORTED;
+
+static int validate(const ipmc_model& m, int64_t n_chains, int& cpl, int& gs) {
+  if (m.q > kBurQMax) {
+    set_error("Burgers: at most %d observation windows", kBurQMax);
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  if (!pick(m.dim, n_chains, cpl, gs)) {
+    set_error("Burgers: N=%d must be a multiple of 4 and at most 512", m.dim);
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  return IPMC_OK;
+}
+
+struct SweepLauncher {
+  const ipmc_model& m;
+  const ipmc_sweep& s;
+  hipStream_t st;
+  template <typename T, int C, int G, bool FM>
+  int operator()() {
+    return launch_sweep<T, C, G, FM>(m, s, st);
+  }
+};
+
+struct EvalLauncher {
+  const ipmc_model& m;
+  int64_t n;
+  const void *u, *y, *ginv;
+  void* out;
+  bool phi;
+  hipStream_t st;
+  template <typename T, int C, int G, bool FM>
+  int operator()() {
+    return launch_eval<T, C, G, FM>(m, n, u, y, ginv, out, phi, st);
+  }
+};
+
+int burgers_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  int cpl, gs;
+  int rc = validate(m, s.n_chains, cpl, gs);
+  if (rc) return rc;
+  SweepLauncher l{m, s, st};
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (s.dtype == IPMC_F64) return fm ? dispatch<double, true>(cpl, gs, l) : dispatch<double, false>(cpl, gs, l);
+  return fm ? dispatch<float, true>(cpl, gs, l) : dispatch<float, false>(cpl, gs, l);
+}
+
+int burgers_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
+                 void* out, bool phi, hipStream_t st) {
+  int cpl, gs;
+  int rc = validate(m, n, cpl, gs);
+  if (rc) return rc;
+  EvalLauncher l{m, n, u, y, ginv, out, phi, st};
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (dtype == IPMC_F64) return fm ? dispatch<double, true>(cpl, gs, l) : dispatch<double, false>(cpl, gs, l);
+  return fm ? dispatch<float, true>(cpl, gs, l) : dispatch<float, false>(cpl, gs, l);
 }
 
 }  // namespace ipmc

@@ -258,6 +258,10 @@ class BurgersOperator(ObservationOperator):
         self.win_lo = np.searchsorted(xv, p - interval / 2, side="left")  # utilities.py:93-95
         self.win_hi = np.searchsorted(xv, p + interval / 2, side="left")  # utilities.py:96-98
         self.q = len(p)
+        if np.any(self.win_hi - self.win_lo - 1 > 128):
+            raise ValueError("BurgersOperator: a measurement window spans more than 129 cells")
+        if self.q > 64:
+            raise ValueError("BurgersOperator: at most 64 measurement windows")
         self.meas_scale = float(meas_scale)
         if dt_mode not in ("cfl", "fixed"):
             raise ValueError("dt_mode must be 'cfl' or 'fixed'")

@@ -316,3 +316,73 @@ def test_sampler_rejects_host_callables(dev):
     s = MCMCSampler(ConstSteppCNProposer(0.5, GaussianDistribution(np.zeros(2), np.eye(2))), pCNAccepter(pot), 1)
     with pytest.raises(UnsupportedOnDevice):
         s.run(np.zeros(2), 2, 0, 1)
+
+
+# ---------------------------------------------------------------- Burgers
+def _burgers_ops():
+    from ip_mcmc_amd import BurgersOperator
+
+    out = []
+    for arith in ("fma", "reference"):
+        for N in (32, 128, 200, 256):
+            out.append(BurgersOperator(N=N, dt_mode="cfl", arith=arith))
+        out.append(BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000, arith=arith))
+        out.append(BurgersOperator(N=128, dt_mode="fixed", dt=2e-3, n_steps=400, nu=1e-3, arith=arith))
+        out.append(BurgersOperator(N=64, dt_mode="cfl", cfl=0.4, nu=5e-4, arith=arith))
+    return out
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_burgers_forward_potential_bit_exact(dev, orc, dtype):
+    rng = np.random.default_rng(4)
+    for op in _burgers_ops():
+        U = 0.25 * rng.normal(size=(96, 3))
+        U[0] = 0.0
+        U[1] = [3.0, 0.0, 0.0]  # fast left state: violates the fixed-dt CFL guard
+        g = op.forward_device(_t(U, dtype, dev)).cpu().numpy()
+        go = orc.forward(op, U, _np(dtype))
+        assert np.array_equal(g, go, equal_nan=True), (op.N, op.dt_mode, op.arith, np.nanmax(np.abs(g - go)))
+        y = np.nan_to_num(go[0]) + 0.05 * rng.normal(size=op.q)
+        ginv = np.full(op.q, 20.0)
+        from ip_mcmc_amd import EvolutionPotential, GaussianDistribution
+
+        pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(op.q), np.diag(1 / ginv**2)))
+        phi = pot.phi_device(_t(U, dtype, dev)).cpu().numpy()
+        phio = orc.potential(op, U, y, ginv, _np(dtype))
+        assert np.array_equal(phi, phio), (op.N, op.dt_mode, op.arith)
+    fixed = _burgers_ops()[4]
+    gi = orc.forward(fixed, [[3.0, 0.0, 0.0]])
+    assert np.all(np.isnan(gi)), "CFL guard never tripped: test is vacuous"
+
+
+@pytest.mark.parametrize("N", [32, 128, 256])
+def test_burgers_device_matches_reference_fixture(dev, golden, N):
+    """RusanovFVM.integrate + Measurer of the reference, on the GPU, fp64 REFERENCE arith: bit-exact."""
+    from ip_mcmc_amd import BurgersOperator
+
+    op = BurgersOperator(prior_mean=(0.0, 0.0, 0.0), N=N, T=1.0, dt_mode="cfl", arith="reference")
+    g = op.forward_device(_t(golden[f"bur{N}_theta"], torch.float64, dev)).cpu().numpy()
+    assert np.array_equal(g, golden[f"bur{N}_G"])
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_burgers_sweep_bit_exact(dev, orc, dtype):
+    """Config 4 shape (N=256, fixed dt 1e-3 x 1000, beta 0.15) and the CFL scheme with the
+    is_valid_IC box constraint (burgers_wasserstein_chain.py:47-55)."""
+    from ip_mcmc_amd import BurgersOperator
+
+    for op in (BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000),
+               BurgersOperator(N=128, dt_mode="cfl", arith="reference")):
+        rng = np.random.default_rng(12)
+        U0 = 0.25 * rng.normal(size=(64, 3))
+        truth = orc.forward(op, [[0.025 - 1.5, -0.025 - 0.25, -0.02 + 0.5]])[0]
+        y = truth + 0.05 * rng.normal(size=op.q)
+        ginv = np.full(op.q, 1 / 0.05)
+        sq = np.full(3, 0.25)
+        phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
+        U0 = U0.astype(_np(dtype)).astype(np.float64)
+        box = (np.array([-np.inf, -np.inf, -1.0]), np.array([np.inf, np.inf, 1.0]), op.theta0)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.15, 31, 0, 6, dtype, dev, box=box)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.15, 31, 0, 6, dtype, box=box)
+        _assert_same(d, o, (op.N, op.dt_mode))
+        assert o["acc"].sum() > 0

@@ -1,0 +1,98 @@
+"""Multi-process chain sharding on CPU (gloo, world_size 2 and 3).
+
+Each rank owns a contiguous block of global chain ids (shard.chain_range),
+advances it with the CPU oracle (the per-rank compute stand-in: on the GPU box
+the same ranks call libipmc), and the blocks are all-gathered in rank order
+(shard.gather_chains).  The gathered states, accept counts and the ordered
+posterior mean must equal one single-process run bit for bit: the RNG is keyed
+by global chain id, so sharding changes nothing.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+C_TOTAL, K, STEPS = 37, 8, 5
+
+
+def _problem():
+    from ip_mcmc_amd.forward import Lorenz96Operator
+
+    op = Lorenz96Operator(K, 8.0, dt=0.01, n_steps=30)
+    rng = np.random.default_rng(0)
+    U0 = 0.2 * rng.normal(size=(C_TOTAL, K))
+    y = 8.0 + 0.3 * rng.normal(size=K)
+    return op, U0, y, np.full(K, 10.0), np.ones(K)
+
+
+def _run_block(start, stop):
+    import sys
+
+    sys.path.insert(0, REPO)
+    from oracle import oracle as O
+
+    op, U0, y, ginv, sq = _problem()
+    U = np.ascontiguousarray(U0[start:stop])
+    phi = O.potential(op, U, y, ginv)
+    acc = np.zeros(stop - start, dtype=np.int64)
+    O.pcn_sweep(op, U, phi, y, ginv, sq, 0.3, 11, 0, STEPS, accepts=acc, chain_offset=start)
+    return U, phi, acc
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import chain_range, gather_chains, ordered_mean
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = chain_range(C_TOTAL, rank, world)
+    U, phi, acc = _run_block(a, b)
+    Ug = gather_chains(torch.from_numpy(U), C_TOTAL)
+    accg = gather_chains(torch.from_numpy(acc).view(-1, 1), C_TOTAL)
+    mean = ordered_mean(Ug)
+    if rank == 0:
+        np.savez(out_path, U=Ug.numpy(), acc=accg.numpy().ravel(), mean=mean)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_chain_range_partitions():
+    from ip_mcmc_amd.shard import chain_range
+
+    for n in (1, 7, 37, 65536):
+        for w in (1, 2, 3, 8):
+            blocks = [chain_range(n, r, w) for r in range(w)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            assert all(blocks[i][1] == blocks[i + 1][0] for i in range(w - 1))
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_run_equals_single_process(tmp_path, world):
+    from ip_mcmc_amd.shard import ordered_mean
+
+    out = str(tmp_path / "g.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, start_method="spawn")
+    got = np.load(out)
+    U, phi, acc = _run_block(0, C_TOTAL)
+    assert np.array_equal(got["U"], U)
+    assert np.array_equal(got["acc"], acc)
+    assert np.array_equal(got["mean"], ordered_mean(torch.from_numpy(U)))

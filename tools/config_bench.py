@@ -1,0 +1,92 @@
+"""Throughput of the BASELINE configs other than the headline (one GPU).
+
+  python tools/config_bench.py [cfg2 cfg4 cfg4full cfg5 ...]
+
+cfg2     Lorenz-63, 500 RK4 steps, 4 096 chains
+cfg4     Burgers N=256, fixed dt 1e-3 x 1000, 2 048 chains (= 16 384 / 8 GPUs)
+cfg4full Burgers as cfg4 with all 16 384 chains on one GPU
+cfg4cfl  Burgers N=256, reference CFL time stepping, 2 048 chains
+cfg5     Lorenz-96 d=256, 10 000 RK4 steps, 131 072 chains (= 2^20 / 8 GPUs)
+"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ip_mcmc_amd import BurgersOperator, Lorenz63Operator, Lorenz96Operator, _abi  # noqa: E402
+from ip_mcmc_amd._lib import call, lib  # noqa: E402
+
+
+def make(cfg):
+    if cfg == "cfg2":
+        x0 = Lorenz63Operator.spinup(n_steps=1000)
+        op = Lorenz63Operator(x0=x0, dt=0.01, n_steps=500)
+        return op, 4096, 0.2, np.array([1.0, 1.0, np.sqrt(0.1)]), 80 * 500, 1.0
+    if cfg in ("cfg4", "cfg4full", "cfg4cfl"):
+        if cfg == "cfg4cfl":
+            op = BurgersOperator(N=256, dt_mode="cfl")
+        else:
+            op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000)
+        n = 16384 if cfg == "cfg4full" else 2048
+        return op, n, 0.15, np.full(3, 0.25), 30 * 256 * 1000, 0.05
+    if cfg == "cfg5":
+        op = Lorenz96Operator(256, 8.0, dt=0.005, n_steps=10000)
+        return op, 131072, 0.2, np.ones(256), 30 * 256 * 10000, 0.1
+    raise SystemExit(f"unknown config {cfg}")
+
+
+def run(cfg, dtype, steps=3):
+    dev = torch.device("cuda", 0)
+    op, n, beta, sq, flop, gamma = make(cfg)
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
+    m, _ = op.model(dtype, dev)
+    u = torch.zeros((n, op.k), dtype=dtype, device=dev)
+    g0 = op.forward_device(u[:1].clone())[0].double().cpu().numpy()
+    y = t(np.nan_to_num(g0) + gamma * np.random.default_rng(1).normal(size=op.q))
+    gi, sqt = t(np.full(op.q, 1 / gamma)), t(sq)
+    phi = torch.empty(n, dtype=dtype, device=dev)
+    adt = _abi.F64 if dtype == torch.float64 else _abi.F32
+    st = torch.cuda.current_stream(dev).cuda_stream
+    call("ipmc_potential", C.byref(m), adt, n, u.data_ptr(), y.data_ptr(), gi.data_ptr(), phi.data_ptr(), st)
+    acc = torch.zeros(n, dtype=torch.int64, device=dev)
+    s = _abi.IpmcSweep()
+    s.dtype, s.n_chains = adt, n
+    s.u, s.phi, s.accepts = u.data_ptr(), phi.data_ptr(), acc.data_ptr()
+    s.y, s.gamma_inv, s.prior_sqrt = y.data_ptr(), gi.data_ptr(), sqt.data_ptr()
+    s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
+    s.seed, s.n_steps = 5, 1
+    call("ipmc_pcn_sweep", C.byref(m), C.byref(s), st)  # warm-up
+    s.step0 = 1
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record()
+        call("ipmc_pcn_sweep", C.byref(m), C.byref(s), st)
+        b.record()
+        s.step0 += 1
+    torch.cuda.synchronize(dev)
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    res = {
+        "config": cfg,
+        "dtype": str(dtype).split(".")[-1],
+        "chains": n,
+        "ms_per_sweep": ms,
+        "pcn_steps_per_s": n / (ms * 1e-3),
+        "tflops_algorithmic": n * flop / (ms * 1e-3) / 1e12,
+        "accept_rate": float(acc.sum().item()) / (n * (steps + 1)),
+    }
+    if isinstance(op, Lorenz96Operator):
+        res["lanes_per_chain"] = lib().ipmc_auto_lanes(C.byref(m), adt, n)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    cfgs = sys.argv[1:] or ["cfg2", "cfg4", "cfg4full", "cfg4cfl", "cfg5"]
+    for c in cfgs:
+        for dt in (torch.float64, torch.float32):
+            run(c, dt)
