@@ -1,0 +1,6 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 2
+export TMPDIR=/tmp
+tools/gpu_session.sh \
+  "pytest_gpu:1200:python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 -rf -x" \
+  "configs:600:python tools/config_bench.py"
