@@ -53,12 +53,12 @@ def problem():
 
 
 class Workload:
-    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0):
+    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0, d=D, chains_per_lane=0):
         self.dev, self.dtype = dev, dtype
         self.model, self._keep = op.model(dtype, dev)
         t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
-        self.y, self.ginv, self.sq = t(y), t(np.full(D, 1 / GAMMA)), t(np.ones(D))
-        self.u = torch.zeros((n_chains, D), dtype=dtype, device=dev)
+        self.y, self.ginv, self.sq = t(y), t(np.full(d, 1 / GAMMA)), t(np.ones(d))
+        self.u = torch.zeros((n_chains, d), dtype=dtype, device=dev)
         self.phi = torch.empty(n_chains, dtype=dtype, device=dev)
         self.acc = torch.zeros(n_chains, dtype=torch.int64, device=dev)
         self.stream = torch.cuda.current_stream(dev).cuda_stream
@@ -66,14 +66,16 @@ class Workload:
         call("ipmc_potential", C.byref(self.model), adt, n_chains, self.u.data_ptr(), self.y.data_ptr(),
              self.ginv.data_ptr(), self.phi.data_ptr(), self.stream)
         s = _abi.IpmcSweep()
-        s.dtype, s.lanes_per_chain = adt, lanes
+        s.dtype, s.lanes_per_chain, s.chains_per_lane = adt, lanes, chains_per_lane
         s.n_chains, s.chain_offset = n_chains, chain_offset
         s.u, s.phi, s.accepts = self.u.data_ptr(), self.phi.data_ptr(), self.acc.data_ptr()
         s.y, s.gamma_inv, s.prior_sqrt = self.y.data_ptr(), self.ginv.data_ptr(), self.sq.data_ptr()
         s.beta, s.contraction = BETA, float(np.sqrt(1 - BETA**2))
         s.seed, s.step0, s.n_steps = 2, 0, 1
         self.s = s
-        self.lanes = call_auto(self.model, adt, n_chains) if lanes == 0 else lanes
+        auto = call_auto(self.model, adt, n_chains)
+        self.lanes = auto % 100 if lanes == 0 else lanes
+        self.chains_per_lane = auto // 100 if chains_per_lane == 0 else chains_per_lane
 
     def step(self):
         call("ipmc_pcn_sweep", C.byref(self.model), C.byref(self.s), self.stream)
@@ -83,7 +85,7 @@ class Workload:
 def call_auto(model, adt, n):
     from ip_mcmc_amd._lib import lib
 
-    return lib().ipmc_auto_lanes(C.byref(model), adt, n)
+    return lib().ipmc_auto_layout(C.byref(model), adt, n)
 
 
 def log(msg):
@@ -231,6 +233,7 @@ def main():
                 "beta": BETA,
                 "arith": "fma",
                 "lanes_per_chain": w.lanes,
+                "chains_per_lane": w.chains_per_lane,
                 "parallelism": f"chains sharded over {world} GPU(s)",
             },
             "roofline": {

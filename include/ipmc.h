@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 1
+#define IPMC_ABI_VERSION 2
 
 typedef enum {
   IPMC_OK = 0,
@@ -101,6 +101,8 @@ typedef struct ipmc_model {
 typedef struct ipmc_sweep {
   int32_t dtype;            /* ipmc_dtype of u/phi/y/gamma_inv/prior_sqrt/box_* */
   int32_t lanes_per_chain;  /* 0 = auto; otherwise a divisor of the state dim (kernel layout only: results are identical) */
+  int32_t chains_per_lane;  /* 0 = auto; 2 = two fp32 chains packed per lane group (v_pk_*_f32), 1 = one (layout only) */
+  int32_t reserved0;
   int64_t n_chains;
   int64_t chain_offset;     /* global id of chain 0 of this shard (RNG counter) */
   void* u;                  /* [n_chains, k] in/out current state */
@@ -146,8 +148,10 @@ int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t 
 int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out,
                  void* stream);
 
-/* Lanes per chain the sweep kernel would use for this model/dtype when lanes_per_chain = 0. */
+/* Layout the sweep kernel would use for this model/dtype when lanes_per_chain = chains_per_lane = 0:
+   returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout. */
 int ipmc_auto_lanes(const ipmc_model* model, int32_t dtype, int64_t n_chains);
+int ipmc_auto_layout(const ipmc_model* model, int32_t dtype, int64_t n_chains);
 
 const char* ipmc_last_error(void);
 int ipmc_abi_version(void);

@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -51,6 +51,8 @@ class IpmcSweep(C.Structure):
     _fields_ = [
         ("dtype", C.c_int32),
         ("lanes_per_chain", C.c_int32),
+        ("chains_per_lane", C.c_int32),
+        ("reserved0", C.c_int32),
         ("n_chains", C.c_int64),
         ("chain_offset", C.c_int64),
         ("u", C.c_void_p),
@@ -90,6 +92,7 @@ SIGNATURES = {
     ),
     "ipmc_uniform": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "ipmc_auto_lanes": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
+    "ipmc_auto_layout": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_last_error": (C.c_char_p, []),
     "ipmc_abi_version": (C.c_int, []),
 }

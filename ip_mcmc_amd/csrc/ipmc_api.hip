@@ -58,21 +58,38 @@ static int check_model(const ipmc_model* m) {
   return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
 }
 
-static bool l96_has(int D, int dtype, int lpc) {
-  return dtype == IPMC_F64 ? l96_has_f64(D, lpc) : l96_has_f32(D, lpc);
+static bool l96_has(int D, int dtype, int lpc, int cpl) {
+  if (dtype == IPMC_F64) return cpl == 1 && l96_has_f64(D, lpc);
+  return l96_has_f32(D, lpc, cpl);
 }
 
-// Smallest lane count that puts >= 2 waves on every SIMD (1024 SIMDs on
-// MI355X: 131072 lanes), else the largest compiled one.
-static int l96_auto(int D, int dtype, int64_t n_chains) {
+// Layout choice for Lorenz-96 (lanes per chain, chains per lane group).
+// fp32 packs two chains per lane group (every FLOP a v_pk_*_f32).  The lane
+// count is the smallest that keeps M = d/LPC <= 10 components per lane (6
+// live arrays of M fit ~3 waves/SIMD without spills), raised while the
+// ensemble would leave SIMDs without 2 waves (1024 SIMDs: 131072 lanes),
+// as long as M stays >= 4 (the halo exchange is 3 values per RHS).
+static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   static const int cands[5] = {1, 2, 4, 8, 16};
-  int best = 0;
+  cpl = (dtype == IPMC_F32) ? 2 : 1;
+  const int64_t groups = (n_chains + cpl - 1) / cpl;
+  lpc = 0;
   for (int i = 0; i < 5; ++i) {
-    if (!l96_has(D, dtype, cands[i])) continue;
-    best = cands[i];
-    if (n_chains * cands[i] >= 131072) return cands[i];
+    const int l = cands[i];
+    if (!l96_has(D, dtype, l, cpl)) continue;
+    if (lpc == 0) lpc = l;  // smallest compiled
+    if (D / l <= 10) {
+      lpc = l;
+      break;
+    }
+    lpc = l;  // keep the largest compiled while M > 10
   }
-  return best;
+  for (int i = 0; i < 5 && lpc; ++i) {
+    const int l = cands[i];
+    if (l <= lpc || !l96_has(D, dtype, l, cpl)) continue;
+    if (groups * lpc >= 131072 || D / l < 4) break;
+    lpc = l;
+  }
 }
 
 template <typename T, int MODEL, bool FM>
@@ -149,8 +166,9 @@ static int dispatch_eval(const ipmc_model* m, int32_t dtype, int64_t n, const vo
       return dtype == IPMC_F64 ? small_eval<double>(*m, n, u, y, ginv, out, phi, st)
                                : small_eval<float>(*m, n, u, y, ginv, out, phi, st);
     case IPMC_MODEL_LORENZ96: {
-      const int lpc = l96_auto(m->dim, dtype, n);
-      if (!lpc) return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: no kernel compiled for this dim");
+      int lpc, cpl;
+      l96_layout(m->dim, IPMC_F64, n, lpc, cpl);  // eval kernels run one chain per lane group
+      if (!lpc || !l96_has(m->dim, dtype, lpc, 1)) return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: no kernel compiled for this dim");
       return dtype == IPMC_F64 ? l96_eval_f64(*m, n, u, y, ginv, out, phi, lpc, st)
                                : l96_eval_f32(*m, n, u, y, ginv, out, phi, lpc, st);
     }
@@ -171,9 +189,17 @@ int ipmc_abi_version(void) { return IPMC_ABI_VERSION; }
 const char* ipmc_last_error(void) { return g_err; }
 
 int ipmc_auto_lanes(const ipmc_model* m, int32_t dtype, int64_t n_chains) {
+  return ipmc_auto_layout(m, dtype, n_chains) % 100;
+}
+
+int ipmc_auto_layout(const ipmc_model* m, int32_t dtype, int64_t n_chains) {
   if (!m) return 0;
-  if (m->kind == IPMC_MODEL_LORENZ96) return l96_auto(m->dim, dtype, n_chains);
-  return 1;
+  if (m->kind == IPMC_MODEL_LORENZ96) {
+    int lpc, cpl;
+    l96_layout(m->dim, dtype, n_chains, lpc, cpl);
+    return cpl * 100 + lpc;
+  }
+  return 101;
 }
 
 int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
@@ -202,16 +228,19 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   switch (m->kind) {
     case IPMC_MODEL_LINEAR:
     case IPMC_MODEL_LORENZ63:
-      if (s->lanes_per_chain > 1) return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane");
+      if (s->lanes_per_chain > 1 || s->chains_per_lane > 1)
+        return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane");
       return s->dtype == IPMC_F64 ? small_sweep<double>(*m, *s, st) : small_sweep<float>(*m, *s, st);
     case IPMC_MODEL_LORENZ96: {
-      int lpc = s->lanes_per_chain;
-      if (lpc == 0) lpc = l96_auto(m->dim, s->dtype, s->n_chains);
-      if (!lpc || !l96_has(m->dim, s->dtype, lpc)) {
-        set_error("Lorenz-96: no kernel compiled for dim=%d lanes_per_chain=%d", m->dim, lpc);
+      int lpc, cpl;
+      l96_layout(m->dim, s->dtype, s->n_chains, lpc, cpl);
+      if (s->chains_per_lane) cpl = s->chains_per_lane;
+      if (s->lanes_per_chain) lpc = s->lanes_per_chain;
+      if (!lpc || !l96_has(m->dim, s->dtype, lpc, cpl)) {
+        set_error("Lorenz-96: no kernel compiled for dim=%d lanes_per_chain=%d chains_per_lane=%d", m->dim, lpc, cpl);
         return IPMC_ERR_UNSUPPORTED;
       }
-      return s->dtype == IPMC_F64 ? l96_sweep_f64(*m, *s, lpc, st) : l96_sweep_f32(*m, *s, lpc, st);
+      return s->dtype == IPMC_F64 ? l96_sweep_f64(*m, *s, lpc, st) : l96_sweep_f32(*m, *s, lpc, cpl, st);
     }
     case IPMC_MODEL_BURGERS:
       return burgers_sweep(*m, *s, st);

@@ -170,16 +170,57 @@ __device__ __forceinline__ float dpp(float v) { return dpp_f32<CTRL>(v); }
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) { return dpp_f64<CTRL>(v); }
 
+// Two fp32 chains packed per lane (x = chain 2p, y = chain 2p+1): every
+// arithmetic op is a v_pk_*_f32 with per-component IEEE semantics, i.e. the
+// same bits as two scalar evaluations.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <bool FM>
+__device__ __forceinline__ f32x2 madd(f32x2 a, f32x2 b, f32x2 c) {
+  if constexpr (FM) return __builtin_elementwise_fma(a, b, c);
+  else return c + a * b;
+}
+template <int CTRL>
+__device__ __forceinline__ f32x2 dpp(f32x2 v) {
+  f32x2 r;
+  r.x = dpp_f32<CTRL>(v.x);
+  r.y = dpp_f32<CTRL>(v.y);
+  return r;
+}
+
 __device__ __forceinline__ float shfl(float v, int src) { return __shfl(v, src, 64); }
 __device__ __forceinline__ double shfl(double v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ f32x2 shfl(f32x2 v, int src) {
+  f32x2 r;
+  r.x = __shfl(v.x, src, 64);
+  r.y = __shfl(v.y, src, 64);
+  return r;
+}
+
+// scalar -> storage type (splat for packed pairs)
+template <typename V>
+struct Splat {
+  template <typename S>
+  __device__ static __forceinline__ V of(S s) { return (V)s; }
+};
+template <>
+struct Splat<f32x2> {
+  __device__ static __forceinline__ f32x2 of(float s) { return f32x2{s, s}; }
+};
 
 // Value of `v` held by the previous / next lane of this chain's lane group
 // (cyclic inside the group of LPC lanes; groups are LPC-aligned).
+// DPP row rotations (rows of 16 lanes): row_ror:1 makes lane i read lane
+// (i-1) mod 16 of its row, row_ror:15 lane (i+1) mod 16.
+constexpr int kRowRor1 = 0x121;
+constexpr int kRowRor15 = 0x12F;
+
 template <int LPC, typename T>
 __device__ __forceinline__ T group_prev(T v, int lane) {
   if constexpr (LPC == 1) return v;
   else if constexpr (LPC == 2) return dpp<qperm(1, 0, 3, 2)>(v);
   else if constexpr (LPC == 4) return dpp<qperm(3, 0, 1, 2)>(v);
+  else if constexpr (LPC == 16) return dpp<kRowRor1>(v);
   else return shfl(v, (lane & ~(LPC - 1)) | ((lane - 1) & (LPC - 1)));
 }
 template <int LPC, typename T>
@@ -187,6 +228,7 @@ __device__ __forceinline__ T group_next(T v, int lane) {
   if constexpr (LPC == 1) return v;
   else if constexpr (LPC == 2) return dpp<qperm(1, 0, 3, 2)>(v);
   else if constexpr (LPC == 4) return dpp<qperm(1, 2, 3, 0)>(v);
+  else if constexpr (LPC == 16) return dpp<kRowRor15>(v);
   else return shfl(v, (lane & ~(LPC - 1)) | ((lane + 1) & (LPC - 1)));
 }
 // Value of `v` held by lane `s` of this chain's group.

@@ -12,13 +12,13 @@ int check_launch(const char* what);
 
 // Lorenz-96 dispatch (ipmc_l96_f32.hip / ipmc_l96_f64.hip).
 // Returns IPMC_ERR_UNSUPPORTED when (D, lpc) has no instantiation.
-int l96_sweep_f32(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st);
+int l96_sweep_f32(const ipmc_model& m, const ipmc_sweep& s, int lpc, int cpl, hipStream_t st);
 int l96_sweep_f64(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st);
 int l96_eval_f32(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
                  int lpc, hipStream_t st);
 int l96_eval_f64(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
                  int lpc, hipStream_t st);
-bool l96_has_f32(int D, int lpc);
+bool l96_has_f32(int D, int lpc, int cpl);  // cpl: chains per lane group (1, or 2 packed)
 bool l96_has_f64(int D, int lpc);
 
 // Burgers (ipmc_burgers.hip)

@@ -39,38 +39,42 @@ __device__ __forceinline__ void l96_rhs(const T (&s)[M], const T (&F)[M], T (&o)
 }
 
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
-template <typename T, int M, int LPC, bool FM>
-__device__ __forceinline__ void l96_forward(const T (&F)[M], const T* __restrict__ x0, T h, int nsteps, int lane,
-                                            T (&g)[M]) {
-  const T h2 = h * (T)0.5;
-  const T h6 = h / (T)6;
-  T x[M], ob[M];
+// V is the per-lane storage type (float, double, or f32x2 = two fp32 chains),
+// S the scalar type of the problem constants.
+template <typename V, int M, int LPC, bool FM, typename S>
+__device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict__ x0, V h, int nsteps, int lane,
+                                            V (&g)[M]) {
+  using P = Splat<V>;
+  const V h2 = h * P::of((S)0.5);
+  const V h6 = h / P::of((S)6);
+  const V two = P::of((S)2);
+  V x[M], ob[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) {
-    x[j] = x0[j];
-    ob[j] = (T)0;
+    x[j] = P::of(x0[j]);
+    ob[j] = P::of((S)0);
   }
   for (int n = 0; n < nsteps; ++n) {
-    T k[M], acc[M], xs[M];
-    l96_rhs<T, M, LPC, FM>(x, F, k, lane);
+    V k[M], acc[M], xs[M];
+    l96_rhs<V, M, LPC, FM>(x, F, k, lane);
 #pragma unroll
     for (int j = 0; j < M; ++j) {
       acc[j] = k[j];
       xs[j] = madd<FM>(h2, k[j], x[j]);
     }
-    l96_rhs<T, M, LPC, FM>(xs, F, k, lane);
+    l96_rhs<V, M, LPC, FM>(xs, F, k, lane);
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-      acc[j] = madd<FM>((T)2, k[j], acc[j]);
+      acc[j] = madd<FM>(two, k[j], acc[j]);
       xs[j] = madd<FM>(h2, k[j], x[j]);
     }
-    l96_rhs<T, M, LPC, FM>(xs, F, k, lane);
+    l96_rhs<V, M, LPC, FM>(xs, F, k, lane);
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-      acc[j] = madd<FM>((T)2, k[j], acc[j]);
+      acc[j] = madd<FM>(two, k[j], acc[j]);
       xs[j] = madd<FM>(h, k[j], x[j]);
     }
-    l96_rhs<T, M, LPC, FM>(xs, F, k, lane);
+    l96_rhs<V, M, LPC, FM>(xs, F, k, lane);
 #pragma unroll
     for (int j = 0; j < M; ++j) {
       acc[j] = acc[j] + k[j];
@@ -78,23 +82,24 @@ __device__ __forceinline__ void l96_forward(const T (&F)[M], const T* __restrict
       ob[j] = ob[j] + x[j];
     }
   }
-  const T nn = (T)nsteps;
+  const V nn = P::of((S)nsteps);
 #pragma unroll
   for (int j = 0; j < M; ++j) g[j] = ob[j] / nn;
 }
 
-template <typename T, int M, int LPC, bool FM>
-__device__ __forceinline__ T l96_potential(const T (&v)[M], const T* __restrict__ th0, const T* __restrict__ x0,
-                                           const T* __restrict__ y, const T* __restrict__ ginv, T h, int nsteps,
+template <typename V, int M, int LPC, bool FM, typename S>
+__device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict__ th0, const S* __restrict__ x0,
+                                           const S* __restrict__ y, const S* __restrict__ ginv, V h, int nsteps,
                                            int lane) {
-  T F[M], g[M];
+  using P = Splat<V>;
+  V F[M], g[M];
 #pragma unroll
-  for (int j = 0; j < M; ++j) F[j] = th0[j] + v[j];
-  l96_forward<T, M, LPC, FM>(F, x0, h, nsteps, lane, g);
-  T r[M];
+  for (int j = 0; j < M; ++j) F[j] = P::of(th0[j]) + v[j];
+  l96_forward<V, M, LPC, FM>(F, x0, h, nsteps, lane, g);
+  V r[M];
 #pragma unroll
-  for (int j = 0; j < M; ++j) r[j] = (y[j] - g[j]) * ginv[j];
-  return (T)0.5 * ordered_sumsq<T, M, LPC, FM>(r, lane, (T)0);
+  for (int j = 0; j < M; ++j) r[j] = (P::of(y[j]) - g[j]) * P::of(ginv[j]);
+  return P::of((S)0.5) * ordered_sumsq<V, M, LPC, FM>(r, lane, P::of((S)0));
 }
 
 constexpr int kL96Block = 256;
@@ -172,6 +177,106 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
     T* so = (T*)s.sample_out + chain * s.sample_stride + c0;
 #pragma unroll
     for (int j = 0; j < M; ++j) so[j] = u[j];
+  }
+}
+
+// fp32, two chains per lane group (x = chain 2p, y = chain 2p+1): the RK loop
+// runs on f32x2 so every FLOP is a v_pk_*_f32; proposal and accept stay per
+// chain (scalar), so the bits equal the one-chain kernel's.
+template <int D, int LPC, bool FM>
+__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<double, D / LPC>())) void l96_sweep_pk_kernel(
+    const ipmc_model m, const ipmc_sweep s) {
+  constexpr int M = D / LPC;
+  using V = f32x2;
+  __shared__ V vpark[M][kL96Block];
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
+  const int64_t pair = tid / LPC;
+  const int sub = (int)(tid % LPC);
+  const int64_t ca = 2 * pair;
+  if (ca >= s.n_chains) return;
+  const bool has_b = ca + 1 < s.n_chains;
+  const int64_t cb = has_b ? ca + 1 : ca;  // a phantom B duplicates A and is never written
+  const uint64_t ga = (uint64_t)(s.chain_offset + ca), gb = (uint64_t)(s.chain_offset + cb);
+  const int c0 = sub * M;
+  float* __restrict__ ua = (float*)s.u + ca * D + c0;
+  float* __restrict__ ub = (float*)s.u + cb * D + c0;
+  const float beta = (float)s.beta, contr = (float)s.contraction;
+  const V h = Splat<V>::of((float)m.dt);
+  float* phi = (float*)s.phi;
+  float pa = phi[ca], pb = phi[cb];
+  int64_t na = 0, nb = 0, ka = 0, kb = 0;
+  for (int64_t st = 0; st < s.n_steps; ++st) {
+    const uint64_t step = s.step0 + (uint64_t)st;
+    int cl = c0;
+    asm volatile("" : "+v"(cl));
+    const float bs = s.beta_schedule ? (float)s.beta_schedule[2 * st] : beta;
+    const float cs = s.beta_schedule ? (float)s.beta_schedule[2 * st + 1] : contr;
+    const float* sq = (const float*)s.prior_sqrt + cl;
+    float va[M], vb[M];
+    pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va);
+    pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb);
+    const bool oka = box_valid<float, M, LPC>(s, c0, va, lane);
+    const bool okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
+    if (oka || okb) {
+      ka += oka;
+      kb += okb;
+      V v[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        v[j] = V{va[j], vb[j]};
+        vpark[j][threadIdx.x] = v[j];
+      }
+      const V ph = l96_potential<V, M, LPC, FM>(v, (const float*)m.theta0 + cl, (const float*)m.x0 + cl,
+                                                (const float*)s.y + cl, (const float*)s.gamma_inv + cl, h,
+                                                m.n_steps, lane);
+      asm volatile("" ::: "memory");
+      if (oka && pcn_accept<float>(pa, ph.x, s.seed, ga, step)) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) ua[j] = vpark[j][threadIdx.x].x;
+        pa = ph.x;
+        ++na;
+      }
+      if (okb && pcn_accept<float>(pb, ph.y, s.seed, gb, step)) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) ub[j] = vpark[j][threadIdx.x].y;
+        pb = ph.y;
+        ++nb;
+      }
+    }
+    if (s.sum_u) {
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const double a = (double)ua[j];
+        s.sum_u[ca * D + c0 + j] += a;
+        if (s.sum_u2) s.sum_u2[ca * D + c0 + j] += a * a;
+        if (has_b) {
+          const double b = (double)ub[j];
+          s.sum_u[cb * D + c0 + j] += b;
+          if (s.sum_u2) s.sum_u2[cb * D + c0 + j] += b * b;
+        }
+      }
+    }
+  }
+  if (sub == 0) {
+    phi[ca] = pa;
+    if (s.accepts) s.accepts[ca] += na;
+    if (s.calls) s.calls[ca] += ka;
+    if (has_b) {
+      phi[cb] = pb;
+      if (s.accepts) s.accepts[cb] += nb;
+      if (s.calls) s.calls[cb] += kb;
+    }
+  }
+  if (s.sample_out) {
+    float* so = (float*)s.sample_out + ca * s.sample_stride + c0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) so[j] = ua[j];
+    if (has_b) {
+      float* sb = (float*)s.sample_out + cb * s.sample_stride + c0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) sb[j] = ub[j];
+    }
   }
 }
 

@@ -52,6 +52,39 @@ int l96_sweep_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t s
   return IPMC_ERR_UNSUPPORTED;
 }
 
+template <int D, int LPC, bool FM>
+int l96_launch_sweep_pk(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  const int64_t pairs = (s.n_chains + 1) / 2;
+  const int64_t blocks = (pairs * LPC + kL96Block - 1) / kL96Block;
+  hipLaunchKernelGGL((l96_sweep_pk_kernel<D, LPC, FM>), dim3((unsigned)blocks), dim3(kL96Block), 0, st, m, s);
+  return check_launch("l96_sweep_pk_kernel");
+}
+
+// packed fp32 pairs: 8 bytes of storage per component, like fp64
+template <int D, bool FM>
+int l96_sweep_pk_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+  switch (lpc) {
+#define IPMC_CASE(L)                                                                     \
+  case L:                                                                                \
+    if constexpr (l96_ok<double, D, L>()) return l96_launch_sweep_pk<D, L, FM>(m, s, st); \
+    break;
+    IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
+#undef IPMC_CASE
+  }
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+inline int l96_sweep_pk(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+  const bool fm = (m.arith == IPMC_ARITH_FMA);
+  switch (m.dim) {
+#define IPMC_DIM(D) \
+  case D: return fm ? l96_sweep_pk_d<D, true>(m, s, lpc, st) : l96_sweep_pk_d<D, false>(m, s, lpc, st);
+    IPMC_L96_DIMS(IPMC_DIM)
+#undef IPMC_DIM
+  }
+  return IPMC_ERR_UNSUPPORTED;
+}
+
 template <typename T, int D, bool FM>
 int l96_eval_d(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
                int lpc, hipStream_t st) {

@@ -157,6 +157,8 @@ int orc_layout(int64_t* out) {
   out[i++] = (int64_t)sizeof(ipmc_sweep);
   out[i++] = (int64_t)offsetof(ipmc_sweep, dtype);
   out[i++] = (int64_t)offsetof(ipmc_sweep, lanes_per_chain);
+  out[i++] = (int64_t)offsetof(ipmc_sweep, chains_per_lane);
+  out[i++] = (int64_t)offsetof(ipmc_sweep, reserved0);
   out[i++] = (int64_t)offsetof(ipmc_sweep, n_chains);
   out[i++] = (int64_t)offsetof(ipmc_sweep, chain_offset);
   out[i++] = (int64_t)offsetof(ipmc_sweep, u);

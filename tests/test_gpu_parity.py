@@ -86,7 +86,7 @@ def test_forward_and_potential_bit_exact(dev, orc, dtype):
 
 # ----------------------------------------------------------------- sweep
 def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, dev, lanes=0, box=None,
-                  sched=None, chain_offset=0, want_sums=False):
+                  sched=None, chain_offset=0, want_sums=False, cpl=0):
     from ip_mcmc_amd import _abi
     from ip_mcmc_amd._lib import call
 
@@ -99,6 +99,7 @@ def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, 
     s = _abi.IpmcSweep()
     s.dtype = _abi.F64 if dtype == torch.float64 else _abi.F32
     s.lanes_per_chain = lanes
+    s.chains_per_lane = cpl
     s.n_chains, s.chain_offset = U.shape[0], chain_offset
     s.u, s.phi, s.accepts, s.calls = U.data_ptr(), phi.data_ptr(), acc.data_ptr(), calls.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = yt.data_ptr(), gt.data_ptr(), st.data_ptr()
@@ -175,20 +176,39 @@ def test_sweep_small_models_bit_exact(dev, orc, dtype):
         assert 0 < o["acc"].sum() < 300 * 25
 
 
-@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-@pytest.mark.parametrize("K,lanes", [(8, 1), (8, 2), (8, 4), (40, 1), (40, 2), (40, 4), (40, 8)])
-def test_sweep_l96_bit_exact_every_layout(dev, orc, dtype, K, lanes):
+@pytest.mark.parametrize("dtype,cpl", [(torch.float64, 1), (torch.float32, 1), (torch.float32, 2)])
+@pytest.mark.parametrize("K,lanes", [(8, 1), (8, 2), (8, 4), (40, 1), (40, 2), (40, 4), (40, 8), (32, 16), (64, 16)])
+def test_sweep_l96_bit_exact_every_layout(dev, orc, dtype, cpl, K, lanes):
+    """Every (lanes per chain, chains per lane) layout gives the oracle's bits;
+    131 chains so the packed fp32 layout has a phantom partner in its last pair."""
     from ip_mcmc_amd import Lorenz96Operator
 
-    if dtype == torch.float64 and K // lanes > 20:
-        pytest.skip("no fp64 instantiation with more than 20 components per lane")
+    if (dtype == torch.float64 or cpl == 2) and K // lanes > 20:
+        pytest.skip("no 8-byte-storage instantiation with more than 20 components per lane")
     for arith in ("fma", "reference"):
         op = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=60, arith=arith)
-        U0, phi0, y, ginv, sq = _problem(op, 130, dtype, orc, seed=K)
-        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype, dev, lanes=lanes)
-        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype)
-        _assert_same(d, o, (K, lanes, arith))
+        U0, phi0, y, ginv, sq = _problem(op, 131, dtype, orc, seed=K)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype, dev, lanes=lanes, cpl=cpl,
+                          want_sums=True)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype, want_sums=True)
+        _assert_same(d, o, (K, lanes, cpl, arith))
         assert np.array_equal(d["samp"], o["u"])
+        assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
+
+
+def test_sweep_l96_d256_subset_bit_exact(dev, orc):
+    """Config 5 shape at reduced length (d=256, 500 RK4 steps, 4096 chains), auto layouts."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    op = Lorenz96Operator(256, 8.0, dt=0.005, n_steps=500)
+    idx = [0, 1, 2, 777, 2048, 4095]
+    for dtype in (torch.float32, torch.float64):
+        U0, phi0, y, ginv, sq = _problem(op, 4096, dtype, orc, seed=2)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.05, 8, 0, 2, dtype, dev)
+        for i in idx:
+            o = _sweep_oracle(orc, op, U0[i:i + 1], phi0[i:i + 1], y, ginv, sq, 0.05, 8, 0, 2, dtype,
+                              chain_offset=i)
+            assert np.array_equal(d["u"][i], o["u"][0]) and d["acc"][i] == o["acc"][0], (dtype, i)
 
 
 def test_sweep_box_schedule_sums_offset(dev, orc):
