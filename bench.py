@@ -88,6 +88,19 @@ def call_auto(model, adt, n):
     return lib().ipmc_auto_layout(C.byref(model), adt, n)
 
 
+def pmc_traffic(dtype, chains):
+    """HBM bytes per launch of the sweep kernel from the committed rocprofv3
+    PMC passes (profiles/r*/pmc_l96_<dtype>.json: FETCH_SIZE x2 + WRITE_SIZE,
+    corrected as MI355X_MICROARCH.md's HBM section prescribes), or None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"pmc_l96_{dtype}.json")), reverse=True):
+        rec = json.load(open(path))
+        if rec.get("chains") == chains and rec.get("d") == D and rec.get("rk4_steps") == N_RK:
+            return rec["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -203,7 +216,7 @@ def main():
     flop = args.chains * FLOP_PER_STEP
     achieved = flop / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    hbm_bytes = args.chains * D * (2 if tdt == torch.float32 else 4) * 2 * 2  # u read+write, sq/y/.. via cache
+    traffic, traffic_src = pmc_traffic(args.dtype, args.chains)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("CPU baseline (C oracle)")
@@ -242,11 +255,15 @@ def main():
                 "peak": peak,
                 "unit": "TFLOP/s",
                 "frac": achieved / peak,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC)",
+                "traffic_source": traffic_src,
+                "hbm_GBps": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9,
+                "hbm_frac": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "kernel_ms": kern_ms,
                 "flop_per_launch": flop,
-                "note": "vector-ALU bound; algorithmic FLOP = 30*d*n per chain-step; "
-                        f"HBM ~{hbm_bytes / (kern_ms * 1e-3) / 1e9:.2f} GB/s of {HBM_PEAK_GBS:.0f}",
+                "note": "vector-ALU (FP64 pipe) bound, no MFMA: algorithmic FLOP = 30*d*n per chain-step; "
+                        "PMC shows the FP64 pipe saturated at ~2.03 GHz (profiles/r1/pmc_l96_f64.json)",
             },
             "cpu_baseline": cpu,
             "accept_rate": accept_rate,
