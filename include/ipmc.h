@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 2
+#define IPMC_ABI_VERSION 3
 
 typedef enum {
   IPMC_OK = 0,
@@ -69,6 +69,8 @@ typedef enum {
 } ipmc_arith;
 
 typedef enum { IPMC_DT_FIXED = 0, IPMC_DT_CFL = 1 } ipmc_dt_mode;
+
+typedef enum { IPMC_PROPOSAL_PCN = 0, IPMC_PROPOSAL_RW = 1 } ipmc_proposal;
 
 /* Forward-map description. Fields not used by a model are ignored. */
 typedef struct ipmc_model {
@@ -119,7 +121,13 @@ typedef struct ipmc_sweep {
   double beta;              /* pCN step size, 0 <= beta <= 1 */
   double contraction;       /* sqrt(1 - beta^2), computed by the host (proposer.py:77) */
   const double* beta_schedule; /* optional [n_steps][2] (beta, contraction) of each step of this launch,
-                                  overriding beta/contraction (VarSteppCNProposer, proposer.py:110-115) */
+                                  overriding beta/contraction (VarSteppCNProposer, proposer.py:110-115;
+                                  VarStepStandardRWProposer, proposer.py:53-56, with beta = sqrt(2)*sqrt(delta(i))) */
+  int32_t proposal;         /* ipmc_proposal: PCN v = contraction*u + beta*w (proposer.py:82),
+                               RW v = u + beta*w (proposer.py:30, beta = sqrt(2 delta)) */
+  int32_t reserved1;
+  const void* reg_scale;    /* optional [k]: accept on I = Φ + ½Σ(reg_scale_i v_i)² instead of Φ
+                               (StandardRWAccepter, accepter.py:98-106); `phi` then caches I(u) */
   uint64_t seed;            /* Philox key */
   uint64_t step0;           /* global pCN step index of the first step of this launch */
   int64_t n_steps;          /* pCN steps in this launch */
@@ -131,6 +139,10 @@ typedef struct ipmc_sweep {
 
 /* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */
 int ipmc_pcn_sweep(const ipmc_model* model, const ipmc_sweep* sweep, void* stream);
+
+/* sweep->phi[c] = the accept potential of sweep->u[c] for every chain: Φ(u), or
+   I(u) = Φ(u) + ½Σ(reg_scale_i u_i)² when sweep->reg_scale is set (call before the first sweep). */
+int ipmc_init_phi(const ipmc_model* model, const ipmc_sweep* sweep, void* stream);
 
 /* Φ(u) for n parameter vectors u [n, k] -> phi [n]  (EvolutionPotential.__call__ minus the constant). */
 int ipmc_potential(const ipmc_model* model, int32_t dtype, int64_t n, const void* u,

@@ -6,13 +6,21 @@ proposal, the forward map G, the potential and the accept/reject fused into
 hand-written HIP kernels for gfx950 (libipmc.so, C-ABI in include/ipmc.h).
 """
 from .sampler import MCMCSampler
-from .proposer import ProposerBase, ConstSteppCNProposer, VarSteppCNProposer
+from .proposer import (
+    ConstStepStandardRWProposer,
+    ConstSteppCNProposer,
+    ProposerBase,
+    PWLinear,
+    VarStepStandardRWProposer,
+    VarSteppCNProposer,
+)
 from .accepter import (
     AccepterBase,
     BoxConstraint,
     ConstrainAccepter,
     CountedAccepter,
     ProbabilisticAccepter,
+    StandardRWAccepter,
     pCNAccepter,
 )
 from .potential import EvolutionPotential, PotentialBase
@@ -32,6 +40,10 @@ __all__ = [
     "ProposerBase",
     "ConstSteppCNProposer",
     "VarSteppCNProposer",
+    "ConstStepStandardRWProposer",
+    "VarStepStandardRWProposer",
+    "PWLinear",
+    "StandardRWAccepter",
     "AccepterBase",
     "BoxConstraint",
     "ConstrainAccepter",

@@ -4,13 +4,14 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
 MODEL_LINEAR, MODEL_LORENZ63, MODEL_LORENZ96, MODEL_BURGERS = 0, 1, 2, 3
 ARITH_FMA, ARITH_REFERENCE = 0, 1
 DT_FIXED, DT_CFL = 0, 1
+PROPOSAL_PCN, PROPOSAL_RW = 0, 1
 
 STATUS_NAMES = {
     OK: "IPMC_OK",
@@ -68,6 +69,9 @@ class IpmcSweep(C.Structure):
         ("beta", C.c_double),
         ("contraction", C.c_double),
         ("beta_schedule", C.c_void_p),
+        ("proposal", C.c_int32),
+        ("reserved1", C.c_int32),
+        ("reg_scale", C.c_void_p),
         ("seed", C.c_uint64),
         ("step0", C.c_uint64),
         ("n_steps", C.c_int64),
@@ -81,6 +85,7 @@ class IpmcSweep(C.Structure):
 # Exported symbols of libipmc.so and their ctypes signatures (include/ipmc.h).
 SIGNATURES = {
     "ipmc_pcn_sweep": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.c_void_p]),
+    "ipmc_init_phi": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.c_void_p]),
     "ipmc_potential": (
         C.c_int,
         [C.POINTER(IpmcModel), C.c_int32, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],

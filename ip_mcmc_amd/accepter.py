@@ -101,6 +101,29 @@ class ProbabilisticAccepter(AccepterBase):
         ...
 
 
+class StandardRWAccepter(ProbabilisticAccepter):
+    """accepter.py:86-106: a(u, v) = exp(I(u) − I(v)),
+    I(w) = Φ(w) + ½‖prior.apply_sqrt_covariance(w)‖².
+
+    The reference applies the sqrt COVARIANCE where its docstring says
+    C^{-1/2} (SURVEY Appendix A, Q6; accepter_test.py:29-30 pins that value);
+    this keeps the reference's behaviour.  On the device the regularizer is
+    ½ Σ_i (sqrt(C_ii) w_i)² (diagonal prior)."""
+
+    def __init__(self, potential, prior):
+        self.theta = potential
+        self.prior = prior
+
+    def accept_probability(self, u, v):
+        Iu = self._I(u)
+        Iv = self._I(v)
+        return np.exp(Iu - Iv)
+
+    def _I(self, w):
+        regularizer = 0.5 * np.linalg.norm(self.prior.apply_sqrt_covariance(w)) ** 2
+        return self.theta(w) + regularizer
+
+
 class pCNAccepter(ProbabilisticAccepter):
     """accepter.py:109-122: a(u, v) = exp(Φ(u) − Φ(v)) (Cotter et al. eq. 4.11)."""
 

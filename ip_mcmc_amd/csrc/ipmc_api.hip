@@ -144,6 +144,14 @@ __global__ void normal_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t 
   out[i] = (T)((j & 1) ? z1 : z0);
 }
 
+// phi[c] = phi[c] + ½ Σ_j (c_j u_cj)²  (the sweep's I = Φ + regularizer, in its order)
+template <typename T, bool FM>
+__global__ void reg_add_kernel(int64_t n, int k, const T* __restrict__ u, const T* __restrict__ c, T* phi) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  phi[i] = phi[i] + small_regularizer<T, FM>(k, c, u + i * k, 1);
+}
+
 __global__ void uniform_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t step, double* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -207,7 +215,10 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   if (rc) return rc;
   if (!s) return fail(IPMC_ERR_INVALID, "sweep is NULL");
   if (s->dtype != IPMC_F32 && s->dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "dtype must be IPMC_F32/F64");
-  if (!(s->beta >= 0.0 && s->beta <= 1.0)) return fail(IPMC_ERR_INVALID, "beta has to be in [0,1]");
+  if (s->proposal != IPMC_PROPOSAL_PCN && s->proposal != IPMC_PROPOSAL_RW)
+    return fail(IPMC_ERR_INVALID, "proposal must be IPMC_PROPOSAL_PCN or IPMC_PROPOSAL_RW");
+  if (s->proposal == IPMC_PROPOSAL_PCN && !(s->beta >= 0.0 && s->beta <= 1.0))
+    return fail(IPMC_ERR_INVALID, "beta has to be in [0,1]");
   if (s->n_chains < 0 || s->n_steps < 0 || s->chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
   if (s->n_chains == 0 || s->n_steps == 0) {
     if (s->n_chains > 0 && s->sample_out) {
@@ -246,6 +257,31 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
       return burgers_sweep(*m, *s, st);
   }
   return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
+}
+
+int ipmc_init_phi(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
+  if (!s) return fail(IPMC_ERR_INVALID, "sweep is NULL");
+  int rc = dispatch_eval(m, s->dtype, s->n_chains, s->u, s->y, s->gamma_inv, s->phi, true, stream);
+  if (rc || !s->reg_scale || s->n_chains == 0) return rc;
+  const int64_t blocks = (s->n_chains + 255) / 256;
+  const bool fm = m->arith == IPMC_ARITH_FMA;
+  hipStream_t st = (hipStream_t)stream;
+  if (s->dtype == IPMC_F64) {
+    if (fm)
+      hipLaunchKernelGGL((reg_add_kernel<double, true>), dim3((unsigned)blocks), dim3(256), 0, st, s->n_chains, m->k,
+                         (const double*)s->u, (const double*)s->reg_scale, (double*)s->phi);
+    else
+      hipLaunchKernelGGL((reg_add_kernel<double, false>), dim3((unsigned)blocks), dim3(256), 0, st, s->n_chains,
+                         m->k, (const double*)s->u, (const double*)s->reg_scale, (double*)s->phi);
+  } else {
+    if (fm)
+      hipLaunchKernelGGL((reg_add_kernel<float, true>), dim3((unsigned)blocks), dim3(256), 0, st, s->n_chains, m->k,
+                         (const float*)s->u, (const float*)s->reg_scale, (float*)s->phi);
+    else
+      hipLaunchKernelGGL((reg_add_kernel<float, false>), dim3((unsigned)blocks), dim3(256), 0, st, s->n_chains,
+                         m->k, (const float*)s->u, (const float*)s->reg_scale, (float*)s->phi);
+  }
+  return check_launch("reg_add_kernel");
 }
 
 int ipmc_potential(const ipmc_model* m, int32_t dtype, int64_t n, const void* u, const void* y,

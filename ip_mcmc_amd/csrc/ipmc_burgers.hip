@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
     const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
     const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
     T v[3];
-    pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v);
+    pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, s.proposal == IPMC_PROPOSAL_RW);
     bool ok = true;
     if (s.box_lo || s.box_hi) {
       const T* lo = (const T*)s.box_lo;
@@ -274,6 +274,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
       ++ncalls;
       T phv = burgers_phi<T, CPL, GS, FM>(m, v, c, row, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
       phv = __shfl(phv, lane & ~(GS - 1), 64);
+      if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
       if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) ur[j] = v[j];

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
   const T beta = (T)s.beta, contr = (T)s.contraction, h = (T)m.dt;
   T* phi = (T*)s.phi;
   T phu = phi[chain];
+  const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
   int64_t nacc = 0, ncalls = 0;
   for (int64_t st = 0; st < s.n_steps; ++st) {
     const uint64_t step = s.step0 + (uint64_t)st;
@@ -141,13 +142,15 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
     const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
     const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
     T v[M];
-    pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v);
+    pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw);
     if (box_valid<T, M, LPC>(s, c0, v, lane)) {
       ++ncalls;
+      const T reg = s.reg_scale ? regularizer<T, M, LPC, FM>((const T*)s.reg_scale + cl, v, lane) : (T)0;
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x] = v[j];
-      const T phv = l96_potential<T, M, LPC, FM>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl,
-                                                 (const T*)s.y + cl, (const T*)s.gamma_inv + cl, h, m.n_steps, lane);
+      T phv = l96_potential<T, M, LPC, FM>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
+                                           (const T*)s.gamma_inv + cl, h, m.n_steps, lane);
+      if (s.reg_scale) phv = phv + reg;  // I(v) = Φ(v) + regularizer (accepter.py:106)
       // memory clobber: re-read v from LDS instead of keeping it live in VGPRs across G
       asm volatile("" ::: "memory");
       if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
@@ -214,8 +217,9 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<double, D / LPC>()))
     const float cs = s.beta_schedule ? (float)s.beta_schedule[2 * st + 1] : contr;
     const float* sq = (const float*)s.prior_sqrt + cl;
     float va[M], vb[M];
-    pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va);
-    pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb);
+    const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
+    pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va, rw);
+    pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb, rw);
     const bool oka = box_valid<float, M, LPC>(s, c0, va, lane);
     const bool okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
     if (oka || okb) {
@@ -223,13 +227,14 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<double, D / LPC>()))
       kb += okb;
       V v[M];
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        v[j] = V{va[j], vb[j]};
-        vpark[j][threadIdx.x] = v[j];
-      }
-      const V ph = l96_potential<V, M, LPC, FM>(v, (const float*)m.theta0 + cl, (const float*)m.x0 + cl,
-                                                (const float*)s.y + cl, (const float*)s.gamma_inv + cl, h,
-                                                m.n_steps, lane);
+      for (int j = 0; j < M; ++j) v[j] = V{va[j], vb[j]};
+      const V reg = s.reg_scale ? regularizer<V, M, LPC, FM>((const float*)s.reg_scale + cl, v, lane) : V{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < M; ++j) vpark[j][threadIdx.x] = v[j];
+      V ph = l96_potential<V, M, LPC, FM>(v, (const float*)m.theta0 + cl, (const float*)m.x0 + cl,
+                                          (const float*)s.y + cl, (const float*)s.gamma_inv + cl, h, m.n_steps,
+                                          lane);
+      if (s.reg_scale) ph = ph + reg;
       asm volatile("" ::: "memory");
       if (oka && pcn_accept<float>(pa, ph.x, s.seed, ga, step)) {
 #pragma unroll

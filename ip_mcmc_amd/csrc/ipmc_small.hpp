@@ -85,6 +85,17 @@ __device__ __forceinline__ T small_potential(const ipmc_model& m, const T* __res
   return (T)0.5 * s;
 }
 
+// ½ Σ_j (c_j v_j)², v strided (StandardRWAccepter regularizer, accepter.py:104-106)
+template <typename T, bool FM>
+__device__ __forceinline__ T small_regularizer(int k, const T* __restrict__ c, const T* __restrict__ v, int vstride) {
+  T s = (T)0;
+  for (int j = 0; j < k; ++j) {
+    const T t = c[j] * v[j * vstride];
+    s = madd<FM>(t, t, s);
+  }
+  return (T)0.5 * s;
+}
+
 template <typename T, int MODEL, bool FM>
 __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
   __shared__ T vpark[kSmallKMax * kSmallBlock];
@@ -101,6 +112,7 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
   T* phi = (T*)s.phi;
   T* v = vpark + threadIdx.x;  // v[j * kSmallBlock]
   T phu = phi[chain];
+  const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
   int64_t nacc = 0, ncalls = 0;
   for (int64_t st = 0; st < s.n_steps; ++st) {
     const uint64_t step = s.step0 + (uint64_t)st;
@@ -111,7 +123,7 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
     for (int j = 0; j < k; ++j) {
       if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
       const T w = sq[j] * (T)((j & 1) ? z1 : z0);
-      const T vj = cs * u[j] + bs * w;
+      const T vj = propose_one<T>(rw, u[j], w, cs, bs);
       v[j * kSmallBlock] = vj;
       const T t = vj + (off ? off[j] : (T)0);
       if (lo && !(lo[j] < t)) ok = false;
@@ -119,8 +131,8 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
     }
     if (ok) {
       ++ncalls;
-      const T phv =
-          small_potential<T, MODEL, FM>(m, v, kSmallBlock, (const T*)s.y, (const T*)s.gamma_inv);
+      T phv = small_potential<T, MODEL, FM>(m, v, kSmallBlock, (const T*)s.y, (const T*)s.gamma_inv);
+      if (s.reg_scale) phv = phv + small_regularizer<T, FM>(k, (const T*)s.reg_scale, v, kSmallBlock);
       if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
         for (int j = 0; j < k; ++j) u[j] = v[j * kSmallBlock];
         phu = phv;

@@ -11,11 +11,18 @@
 
 namespace ipmc {
 
-// v = contraction*u + beta*(sqrt(C_ii) * xi_i)     (proposer.py:81-82; the
-// expression order of the reference: two products, then the sum, no FMA)
+// pCN: v = contraction*u + beta*(sqrt(C_ii) * xi_i)   (proposer.py:81-82)
+// RW:  v = u + beta*(sqrt(C_ii) * xi_i)               (proposer.py:29-30, beta = sqrt(2 delta))
+// in the reference's expression order: products first, then the sum, no FMA.
+template <typename T>
+__device__ __forceinline__ T propose_one(bool rw, T u, T w, T contr, T beta) {
+  return rw ? u + beta * w : contr * u + beta * w;
+}
+
 template <typename T, int M>
 __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __restrict__ sq, T contr, T beta,
-                                            uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M]) {
+                                            uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M],
+                                            bool rw = false) {
   if constexpr (M % 2 == 0) {
     // c0 is even whenever M is even: pairs never straddle lanes
 #pragma unroll
@@ -24,8 +31,8 @@ __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __
       normal_pair(seed, gid, step, (uint32_t)((c0 + j) >> 1), z0, z1);
       const T w0 = sq[j] * (T)z0;
       const T w1 = sq[j + 1] * (T)z1;
-      v[j] = contr * u[j] + beta * w0;
-      v[j + 1] = contr * u[j + 1] + beta * w1;
+      v[j] = propose_one<T>(rw, u[j], w0, contr, beta);
+      v[j + 1] = propose_one<T>(rw, u[j + 1], w1, contr, beta);
     }
   } else {
     double z0 = 0.0, z1 = 0.0;
@@ -34,7 +41,7 @@ __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __
       const int c = c0 + j;
       if (j == 0 || (c & 1) == 0) normal_pair(seed, gid, step, (uint32_t)(c >> 1), z0, z1);
       const T w = sq[j] * (T)((c & 1) ? z1 : z0);
-      v[j] = contr * u[j] + beta * w;
+      v[j] = propose_one<T>(rw, u[j], w, contr, beta);
     }
   }
 }
@@ -53,6 +60,18 @@ __device__ __forceinline__ T ordered_sumsq(const T (&r)[M], int lane, T s) {
     }
     return ordered_sumsq<T, M, LPC, FM, S + 1>(r, lane, s);
   }
+}
+
+// StandardRWAccepter regularizer ½ Σ_i (c_i v_i)² over the chain's components
+// in component order (accepter.py:104-106 with the reference's sqrt-covariance
+// factor); c = reg_scale + this lane's offset.
+template <typename V, int M, int LPC, bool FM, typename S>
+__device__ __forceinline__ V regularizer(const S* __restrict__ c, const V (&v)[M], int lane) {
+  using P = Splat<V>;
+  V t[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) t[j] = P::of(c[j]) * v[j];
+  return P::of((S)0.5) * ordered_sumsq<V, M, LPC, FM>(t, lane, P::of((S)0));
 }
 
 // ConstrainAccepter box: lo < v + off < hi for every component of the chain.

@@ -21,15 +21,83 @@ class ProposerBase(ABC):
         ...
 
 
+class ConstStepStandardRWProposer(ProposerBase):
+    """proposer.py:14-30: v = u + sqrt(2 delta) w, w ~ N(0, C) (Cotter et al. eq. 4.3)."""
+
+    kind = "rw"
+
+    def __init__(self, delta, prior):
+        self.prefactor = np.sqrt(2 * delta)
+        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+
+    def device_step(self):
+        return float(self.prefactor), 1.0
+
+    def beta_schedule(self, i0, n):
+        return None
+
+    def __call__(self, u, rng):
+        return u + self.prefactor * self.w.sample(rng)
+
+
+class VarStepStandardRWProposer(ProposerBase):
+    """proposer.py:33-56: v = u + sqrt(2) sqrt(delta(i)) w with i counted from 1
+    (incremented before use); the sampler passes each launch's step sizes to
+    the kernel (ipmc_sweep.beta_schedule)."""
+
+    kind = "rw"
+
+    def __init__(self, delta, prior):
+        self.prefactor = np.sqrt(2)
+        self.delta = delta
+        self.i = 0
+        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+
+    def beta_schedule(self, i0, n):
+        sched = np.empty((n, 2), dtype=np.float64)
+        sched[:, 0] = [self.prefactor * np.sqrt(self.delta(i0 + j + 1)) for j in range(n)]
+        sched[:, 1] = 1.0
+        return sched
+
+    def __call__(self, u, rng):
+        self.i += 1
+        stepsize = self.prefactor * np.sqrt(self.delta(self.i))
+        return u + stepsize * self.w.sample(rng)
+
+
+class PWLinear:
+    """Piecewise-linear step schedule (report/scripts/burgers/burgers_beta.py:131-147):
+    delta decreases linearly from start_delta until len_burn_in, then stays end_delta."""
+
+    def __init__(self, start_delta, end_delta, len_burn_in):
+        self.d_s = start_delta
+        self.d_e = end_delta
+        self.l = len_burn_in
+        self.slope = (start_delta - end_delta) / len_burn_in
+
+    def __call__(self, i):
+        if i > self.l:
+            return self.d_e
+        return self.d_s - self.slope * i
+
+    def __repr__(self):
+        return f"pwl_{self.d_s}_{self.d_e}_{self.l}"
+
+
 class ConstSteppCNProposer(ProposerBase):
     """proposer.py:59-82.  Only the prior covariance is used; a non-zero prior
     mean is ignored (callers sample perturbations around it, Q1)."""
+
+    kind = "pcn"
 
     def __init__(self, beta, prior):
         assert 0 <= beta <= 1, "beta has to be in [0,1]"
         self.beta = beta
         self.contraction = np.sqrt(1 - beta**2)  # proposer.py:77
         self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+
+    def device_step(self):
+        return float(self.beta), float(self.contraction)
 
     def beta_schedule(self, i0, n):
         """(beta, contraction) for proposals i0+1 .. i0+n (constant here)."""
@@ -43,6 +111,8 @@ class VarSteppCNProposer(ProposerBase):
     """proposer.py:85-115: beta(i) for the i-th proposal, i counted from 1
     (incremented before use, :111-112).  The sampler passes the schedule of
     each launch to the kernel (ipmc_sweep.beta_schedule)."""
+
+    kind = "pcn"
 
     def __init__(self, beta, prior):
         self.beta = beta

@@ -8,7 +8,8 @@ Reference (sampler.py:6-54): ``MCMCSampler(proposal, acceptance, rng)``;
 
 Here ``u_0`` may be one state (k,) — same return shape as the reference — or
 a stack (C, k) of C independent chains, returning (C, n_samples, k).  The
-pCN step (ConstSteppCNProposer / VarSteppCNProposer + pCNAccepter on an
+step (ConstSteppCNProposer / VarSteppCNProposer / ConstStepStandardRWProposer /
+VarStepStandardRWProposer + pCNAccepter or StandardRWAccepter on an
 EvolutionPotential with a device forward map, optionally wrapped in
 CountedAccepter / ConstrainAccepter(BoxConstraint)) runs as one fused HIP
 kernel per block of steps (libipmc ``ipmc_pcn_sweep``).  Any other
@@ -29,9 +30,9 @@ import torch
 from . import _abi
 from . import device as dev
 from ._lib import UnsupportedOnDevice, call
-from .accepter import BoxConstraint, ConstrainAccepter, CountedAccepter, pCNAccepter
+from .accepter import BoxConstraint, ConstrainAccepter, CountedAccepter, StandardRWAccepter, pCNAccepter
+from .distribution import GaussianDistribution
 from .potential import EvolutionPotential
-from .proposer import ConstSteppCNProposer, VarSteppCNProposer
 from .rng import PhiloxRNG, resolve_rng
 
 # pCN steps per chain in one kernel launch (launches are split at sample
@@ -43,17 +44,20 @@ class _Plan:
     """The device form of a proposer/accepter composition."""
 
     def __init__(self, proposer, accepter):
-        if not isinstance(proposer, (ConstSteppCNProposer, VarSteppCNProposer)):
+        if getattr(proposer, "kind", None) not in ("pcn", "rw"):
             raise UnsupportedOnDevice(
-                f"device sampler needs a ConstSteppCNProposer or VarSteppCNProposer, not {type(proposer).__name__}"
+                "device sampler needs a ConstSteppCNProposer, VarSteppCNProposer, ConstStepStandardRWProposer or "
+                f"VarStepStandardRWProposer, not {type(proposer).__name__}"
             )
         if not proposer.w.is_diagonal:
             raise UnsupportedOnDevice("device sampler needs a diagonal prior covariance")
         self.proposer = proposer
+        self.proposal = _abi.PROPOSAL_RW if proposer.kind == "rw" else _abi.PROPOSAL_PCN
         self.prior_sqrt = proposer.w.sqrt_diagonal
         self.counted_outer = []  # CountedAccepters that see every step
         self.counted_inner = []  # CountedAccepters inside a ConstrainAccepter
         self.box = None
+        self.reg_scale = None
         acc, inside = accepter, False
         while True:
             if isinstance(acc, CountedAccepter):
@@ -71,16 +75,26 @@ class _Plan:
                 acc = acc.accepter
             elif isinstance(acc, pCNAccepter):
                 break
+            elif isinstance(acc, StandardRWAccepter):
+                prior = acc.prior
+                if not isinstance(prior, GaussianDistribution) or not prior.is_diagonal:
+                    raise UnsupportedOnDevice("StandardRWAccepter on the device needs a diagonal GaussianDistribution prior")
+                self.reg_scale = prior.sqrt_diagonal  # apply_sqrt_covariance's diagonal (Q6)
+                break
             else:
-                raise UnsupportedOnDevice(f"device sampler needs a pCNAccepter, not {type(acc).__name__}")
+                raise UnsupportedOnDevice(
+                    f"device sampler needs a pCNAccepter or StandardRWAccepter, not {type(acc).__name__}"
+                )
         pot = acc.theta
         if not isinstance(pot, EvolutionPotential):
-            raise UnsupportedOnDevice(f"pCNAccepter on the device needs an EvolutionPotential, not {type(pot).__name__}")
+            raise UnsupportedOnDevice(f"the accepter's potential must be an EvolutionPotential, not {type(pot).__name__}")
         self.potential = pot
         self.G = pot.G
         self.y_eff, self.gamma_inv = pot.device_terms()
         if self.prior_sqrt.shape[0] != self.G.k:
             raise ValueError(f"prior dimension {self.prior_sqrt.shape[0]} != forward map k = {self.G.k}")
+        if self.reg_scale is not None and self.reg_scale.shape[0] != self.G.k:
+            raise ValueError("StandardRWAccepter prior dimension != forward map k")
 
 
 class MCMCSampler:
@@ -137,7 +151,7 @@ class MCMCSampler:
             self.accepter.reset()  # sampler.py:15-16
 
         stream = dev.stream_handle(device)
-        phi = plan.potential.phi_device(U)
+        phi = torch.empty((n_chains,), dtype=td, device=device)
         accepts = torch.zeros((n_chains,), dtype=torch.int64, device=device)
         calls = torch.zeros((n_chains,), dtype=torch.int64, device=device) if plan.counted_inner else None
         y_t = dev.to_device(plan.y_eff, td, device)
@@ -150,6 +164,8 @@ class MCMCSampler:
             ts = [None if a is None else dev.to_device(a, td, device) for a in arrs]
             keep_alive += [t for t in ts if t is not None]
             box_ptrs = tuple(dev.ptr(t) for t in ts)
+        reg_t = None if plan.reg_scale is None else dev.to_device(plan.reg_scale, td, device)
+        keep_alive.append(reg_t)
         model, _ = plan.G.model(td, device)
 
         sw = _abi.IpmcSweep()
@@ -165,11 +181,14 @@ class MCMCSampler:
         sw.gamma_inv = gi_t.data_ptr()
         sw.prior_sqrt = sq_t.data_ptr()
         sw.box_lo, sw.box_hi, sw.box_off = box_ptrs
-        const_beta = isinstance(plan.proposer, ConstSteppCNProposer)
+        sw.proposal = plan.proposal
+        sw.reg_scale = dev.ptr(reg_t)
+        const_beta = hasattr(plan.proposer, "device_step")
         if const_beta:
-            sw.beta = float(plan.proposer.beta)
-            sw.contraction = float(plan.proposer.contraction)
+            sw.beta, sw.contraction = plan.proposer.device_step()
         sw.seed = rng.seed
+        # the accept potential of the starting states: Φ(u), or I(u) for StandardRWAccepter
+        call("ipmc_init_phi", C.byref(model), C.byref(sw), stream)
 
         step = rng.step
         prop_i = getattr(plan.proposer, "i", 0)
@@ -229,7 +248,7 @@ class MCMCSampler:
 
         total = step - rng.step
         rng.step = step
-        if isinstance(plan.proposer, VarSteppCNProposer):
+        if hasattr(plan.proposer, "i"):
             plan.proposer.i = prop_i
 
         acc_np = accepts.cpu().numpy()

@@ -80,7 +80,7 @@ int orc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, int32_t n_threads) {
   int st = check_model(m);
   if (st) return st;
   if (!s || !s->u || !s->phi || !s->y || !s->gamma_inv || !s->prior_sqrt) return IPMC_ERR_INVALID;
-  if (!(s->beta >= 0.0 && s->beta <= 1.0)) return IPMC_ERR_INVALID;
+  if (s->proposal == IPMC_PROPOSAL_PCN && !(s->beta >= 0.0 && s->beta <= 1.0)) return IPMC_ERR_INVALID;
   const int64_t C = s->n_chains;
   if (n_threads < 1) n_threads = 1;
 #pragma omp parallel for num_threads(n_threads) schedule(static)
@@ -92,6 +92,12 @@ int orc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, int32_t n_threads) {
       sweep_range_f32(m, s, b, e);
   }
   return IPMC_OK;
+}
+
+int orc_init_phi(const ipmc_model* m, const ipmc_sweep* s) {
+  int st = check_model(m);
+  if (st) return st;
+  return s->dtype == IPMC_F64 ? init_phi_f64(m, s) : init_phi_f32(m, s);
 }
 
 void orc_normal_batch(uint64_t seed, int64_t chain_offset, int64_t n, uint64_t step, int32_t k, double* out) {
@@ -174,6 +180,9 @@ int orc_layout(int64_t* out) {
   out[i++] = (int64_t)offsetof(ipmc_sweep, beta);
   out[i++] = (int64_t)offsetof(ipmc_sweep, contraction);
   out[i++] = (int64_t)offsetof(ipmc_sweep, beta_schedule);
+  out[i++] = (int64_t)offsetof(ipmc_sweep, proposal);
+  out[i++] = (int64_t)offsetof(ipmc_sweep, reserved1);
+  out[i++] = (int64_t)offsetof(ipmc_sweep, reg_scale);
   out[i++] = (int64_t)offsetof(ipmc_sweep, seed);
   out[i++] = (int64_t)offsetof(ipmc_sweep, step0);
   out[i++] = (int64_t)offsetof(ipmc_sweep, n_steps);

@@ -127,16 +127,21 @@ def pcn_sweep(
     beta_schedule=None,
     sums=None,
     n_threads=1,
+    proposal="pcn",
+    reg_scale=None,
 ):
-    """In-place sweep on numpy arrays U [C, k] and phi [C] (dtype from U)."""
+    """In-place sweep on numpy arrays U [C, k] and phi [C] (dtype from U).
+    proposal 'pcn': v = sqrt(1-beta^2) u + beta w; 'rw': v = u + beta w.
+    reg_scale: StandardRWAccepter regularizer scale (phi then holds I)."""
     npd = U.dtype.type
     assert U.flags.c_contiguous and phi.dtype == U.dtype
     m, keep = model_struct(op, npd)
     cv = lambda a: None if a is None else np.ascontiguousarray(np.asarray(a, dtype=np.float64).astype(npd))
     y, gi, sq = cv(y), cv(ginv), cv(prior_sqrt)
     lo, hi, off = (cv(b) for b in box)
+    rs = cv(reg_scale)
     sched = None if beta_schedule is None else np.ascontiguousarray(beta_schedule, dtype=np.float64)
-    keep += [y, gi, sq, lo, hi, off, sched]
+    keep += [y, gi, sq, lo, hi, off, sched, rs]
     s = _abi.IpmcSweep()
     s.dtype = _abi_dtype(npd)
     s.n_chains = U.shape[0]
@@ -148,8 +153,10 @@ def pcn_sweep(
     s.y, s.gamma_inv, s.prior_sqrt = _p(y), _p(gi), _p(sq)
     s.box_lo, s.box_hi, s.box_off = _p(lo), _p(hi), _p(off)
     s.beta = float(beta)
-    s.contraction = float(np.sqrt(1 - beta**2))
+    s.contraction = float(np.sqrt(1 - beta**2)) if proposal == "pcn" else 1.0
     s.beta_schedule = _p(sched)
+    s.proposal = _abi.PROPOSAL_RW if proposal == "rw" else _abi.PROPOSAL_PCN
+    s.reg_scale = _p(rs)
     s.seed = seed
     s.step0 = step0
     s.n_steps = n_steps
@@ -157,6 +164,23 @@ def pcn_sweep(
         s.sum_u, s.sum_u2 = _p(sums[0]), _p(sums[1])
     rc = lib().orc_pcn_sweep(C.byref(m), C.byref(s), n_threads)
     assert rc == 0, rc
+
+
+def init_phi(op, U, y, ginv, reg_scale=None):
+    """phi[c] = Φ(U_c) (+ ½Σ(reg_scale_i U_ci)²), the sweep's accept potential."""
+    npd = U.dtype.type
+    m, keep = model_struct(op, npd)
+    cv = lambda a: None if a is None else np.ascontiguousarray(np.asarray(a, dtype=np.float64).astype(npd))
+    y, gi, rs = cv(y), cv(ginv), cv(reg_scale)
+    phi = np.empty(U.shape[0], dtype=npd)
+    s = _abi.IpmcSweep()
+    s.dtype = _abi_dtype(npd)
+    s.n_chains = U.shape[0]
+    s.u, s.phi, s.y, s.gamma_inv, s.reg_scale = _p(U), _p(phi), _p(y), _p(gi), _p(rs)
+    lib().orc_init_phi.argtypes = [C.POINTER(_abi.IpmcModel), C.POINTER(_abi.IpmcSweep)]
+    rc = lib().orc_init_phi(C.byref(m), C.byref(s))
+    assert rc == 0, rc
+    return phi
 
 
 def normals(seed, chain_offset, n, step, k):

@@ -40,7 +40,10 @@ matplotlib.use("Agg")
 import ip_mcmc  # noqa: E402
 from ip_mcmc import (  # noqa: E402
     ConstrainAccepter,
+    ConstStepStandardRWProposer,
     ConstSteppCNProposer,
+    StandardRWAccepter,
+    VarStepStandardRWProposer,
     CountedAccepter,
     EvolutionPotential,
     GaussianDistribution,
@@ -96,12 +99,12 @@ class RecordingAccepter:
 
 
 def run_reference_chain(G, y, noise_cov_diag, prior_var_diag, beta, u0, seed, chain, n_samples, burn_in, interval,
-                        box=None):
+                        box=None, proposer=None, rw_accept=False):
     prior = GaussianDistribution(mean=np.zeros(len(u0)), covariance=np.diag(prior_var_diag))
     noise = GaussianDistribution(mean=np.zeros(len(y)), covariance=np.diag(noise_cov_diag))
     pot = EvolutionPotential(G, y, noise)
-    prop = ConstSteppCNProposer(beta, prior)
-    inner = CountedAccepter(pCNAccepter(pot))
+    prop = ConstSteppCNProposer(beta, prior) if proposer is None else proposer(prior)
+    inner = CountedAccepter(StandardRWAccepter(pot, prior) if rw_accept else pCNAccepter(pot))
     rec = RecordingAccepter(inner)
     acc = rec if box is None else ConstrainAccepter(rec, box)
     rng = CounterRNG(seed, chain)
@@ -229,6 +232,48 @@ def make_linear(out):
     out["lin_phi"] = np.array([pot(u) for u in U])
 
 
+def pw_linear(d_s, d_e, l):
+    """The harness's step schedule, the formula of burgers_beta.py:131-147's PWLinear
+    (that script cannot be imported here: it pulls in helpers.py, which needs POT)."""
+    slope = (d_s - d_e) / l
+    return lambda i: d_e if i > l else d_s - slope * i
+
+
+def make_rw(out):
+    """Random-walk chains (proposer.py:14-56 + accepter.py:86-106, the §8(f) #1
+    composition of burgers_beta.py:104-128) through the reference sampler."""
+    g = np.array([3.0, 1.0, 4.0, 1.0])
+    gamma = 0.5
+    y = np.array([np.dot(g, [2.0, 7.0, 1.0, 8.0]) + 0.2])
+    prior_var = np.array([0.5, 2.0, 1.0, 1.5])
+    seed = 777
+
+    def G(u):
+        return np.dot(g, u)
+
+    cases = {
+        "const": lambda prior: ConstStepStandardRWProposer(0.05, prior),
+        "var": lambda prior: VarStepStandardRWProposer(pw_linear(0.1, 0.001, 60), prior),
+    }
+    for name, mk in cases.items():
+        res = []
+        for chain in range(3):
+            s, dec, steps, calls, accepts = run_reference_chain(
+                G, y, np.array([gamma**2]), prior_var, None, np.zeros(4), seed, chain, n_samples=20, burn_in=60,
+                interval=10, proposer=mk, rw_accept=True)
+            res.append((s, calls, accepts))
+        out[f"rw_{name}_samples"] = np.stack([r[0] for r in res])
+        out[f"rw_{name}_counts"] = np.array([[r[1], r[2]] for r in res])
+    out["rw_g"], out["rw_y"], out["rw_prior_var"] = g, y, prior_var
+    out["rw_meta"] = np.array([gamma, seed, 20, 60, 10, 0.05, 0.1, 0.001, 60], dtype=np.float64)
+    # StandardRWAccepter._I values (accepter.py:104-106) on random points
+    prior = GaussianDistribution(np.zeros(4), np.diag(prior_var))
+    acc = StandardRWAccepter(EvolutionPotential(G, y, GaussianDistribution(0, gamma**2)), prior)
+    U = np.random.default_rng(8).normal(size=(12, 4))
+    out["rw_I_u"] = U
+    out["rw_I"] = np.array([acc._I(u) for u in U])
+
+
 # ---------------------------------------------------------------- Burgers
 def burgers_flux(w):
     return 0.5 * w * w  # utilities.py:114-115 (BurgersEquation.flux)
@@ -327,6 +372,7 @@ def main():
     make_l96(out)
     make_l96_chain(out)
     make_linear(out)
+    make_rw(out)
     make_burgers(out)
     make_misc(out)
     path = os.path.join(HERE, "reference_golden.npz")

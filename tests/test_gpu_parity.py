@@ -86,9 +86,11 @@ def test_forward_and_potential_bit_exact(dev, orc, dtype):
 
 # ----------------------------------------------------------------- sweep
 def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, dev, lanes=0, box=None,
-                  sched=None, chain_offset=0, want_sums=False, cpl=0):
+                  sched=None, chain_offset=0, want_sums=False, cpl=0, proposal="pcn", reg_scale=None):
     from ip_mcmc_amd import _abi
     from ip_mcmc_amd._lib import call
+
+    rs_t = None if reg_scale is None else _t(reg_scale, dtype, dev)
 
     U = _t(U0, dtype, dev)
     phi = _t(phi0, dtype, dev)
@@ -112,7 +114,9 @@ def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, 
         sc = torch.as_tensor(sched).to(dev)
         keep.append(sc)
         s.beta_schedule = sc.data_ptr()
-    s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
+    s.beta, s.contraction = beta, (float(np.sqrt(1 - beta**2)) if proposal == "pcn" else 1.0)
+    s.proposal = _abi.PROPOSAL_RW if proposal == "rw" else _abi.PROPOSAL_PCN
+    s.reg_scale = None if rs_t is None else rs_t.data_ptr()
     s.seed, s.step0, s.n_steps = seed, step0, n_steps
     samp = torch.zeros_like(U)
     s.sample_out, s.sample_stride = samp.data_ptr(), U.shape[1]
@@ -131,7 +135,7 @@ def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, 
 
 
 def _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, box=None, sched=None,
-                  chain_offset=0, want_sums=False):
+                  chain_offset=0, want_sums=False, proposal="pcn", reg_scale=None):
     npd = _np(dtype)
     U = np.ascontiguousarray(U0.astype(npd))
     phi = np.ascontiguousarray(phi0.astype(npd))
@@ -140,7 +144,7 @@ def _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dt
     sums = (np.zeros(U.shape), np.zeros(U.shape)) if want_sums else None
     orc.pcn_sweep(op, U, phi, y, ginv, sq, beta, seed, step0, n_steps, accepts=acc, calls=calls,
                   chain_offset=chain_offset, box=box or (None, None, None), beta_schedule=sched, sums=sums,
-                  n_threads=8)
+                  n_threads=8, proposal=proposal, reg_scale=reg_scale)
     out = dict(u=U, phi=phi, acc=acc, calls=calls)
     if want_sums:
         out["sum_u"], out["sum_u2"] = sums
@@ -406,3 +410,73 @@ def test_burgers_sweep_bit_exact(dev, orc, dtype):
         o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.15, 31, 0, 6, dtype, box=box)
         _assert_same(d, o, (op.N, op.dt_mode))
         assert o["acc"].sum() > 0
+
+
+# ------------------------------------------------- random walk (§8(f) #1)
+def test_rw_sweeps_bit_exact(dev, orc):
+    """RW proposal + StandardRWAccepter regularizer, const and scheduled step
+    sizes, on every kernel family (small, Lorenz-96 incl. packed fp32, Burgers)."""
+    from ip_mcmc_amd import BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator
+
+    rng = np.random.default_rng(17)
+    ops = [LinearOperator(rng.normal(size=(2, 4))), Lorenz63Operator(x0=(1.0, 2.0, 20.0), n_steps=200),
+           Lorenz96Operator(40, 8.0, dt=0.005, n_steps=50), BurgersOperator(N=64, dt_mode="cfl")]
+    for op in ops:
+        for dtype, cpl in ((torch.float64, 0), (torch.float32, 1), (torch.float32, 2)):
+            if cpl and not isinstance(op, Lorenz96Operator):
+                continue
+            U0, phi0, y, ginv, sq = _problem(op, 70, dtype, orc, seed=3)
+            rs = 0.5 + rng.random(op.k)
+            phi0 = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
+            n = 5
+            sched = np.stack([np.linspace(0.05, 0.2, n), np.ones(n)], axis=1)
+            for sc in (None, sched):
+                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.1, 4, 3, n, dtype, dev, sched=sc, cpl=cpl,
+                                  proposal="rw", reg_scale=rs)
+                o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.1, 4, 3, n, dtype, sched=sc, proposal="rw",
+                                  reg_scale=rs)
+                _assert_same(d, o, (type(op).__name__, dtype, cpl, sc is None))
+
+
+def test_init_phi_with_regularizer_bit_exact(dev, orc):
+    from ip_mcmc_amd import Lorenz96Operator, _abi
+    from ip_mcmc_amd._lib import call
+
+    op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=40)
+    for dtype in (torch.float64, torch.float32):
+        U0, phi0, y, ginv, sq = _problem(op, 90, dtype, orc, seed=6)
+        rs = np.linspace(0.5, 2.0, 40)
+        want = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs)
+        U, yt, gt, rt = _t(U0, dtype, dev), _t(y, dtype, dev), _t(ginv, dtype, dev), _t(rs, dtype, dev)
+        phi = torch.empty(90, dtype=dtype, device=dev)
+        m, _ = op.model(dtype, dev)
+        s = _abi.IpmcSweep()
+        s.dtype = _abi.F64 if dtype == torch.float64 else _abi.F32
+        s.n_chains, s.u, s.phi = 90, U.data_ptr(), phi.data_ptr()
+        s.y, s.gamma_inv, s.reg_scale = yt.data_ptr(), gt.data_ptr(), rt.data_ptr()
+        call("ipmc_init_phi", C.byref(m), C.byref(s), _stream(dev))
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(phi.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("kind", ["const", "var"])
+def test_sampler_rw_matches_reference_fixture(dev, golden, kind):
+    """Reference RW sampler (ConstStep/VarStepStandardRWProposer + CountedAccepter(StandardRWAccepter))
+    with injected draws, reproduced through MCMCSampler on the GPU."""
+    from ip_mcmc_amd import (ConstStepStandardRWProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             LinearOperator, MCMCSampler, PhiloxRNG, PWLinear, StandardRWAccepter,
+                             VarStepStandardRWProposer)
+
+    meta = golden["rw_meta"]
+    gamma, seed, n_samples, burn_in, interval = meta[0], int(meta[1]), int(meta[2]), int(meta[3]), int(meta[4])
+    prior = GaussianDistribution(np.zeros(4), np.diag(golden["rw_prior_var"]))
+    pot = EvolutionPotential(LinearOperator(golden["rw_g"], arith="reference"), golden["rw_y"],
+                             GaussianDistribution(0, gamma**2))
+    for chain in range(3):
+        prop = (ConstStepStandardRWProposer(meta[5], prior) if kind == "const"
+                else VarStepStandardRWProposer(PWLinear(meta[6], meta[7], int(meta[8])), prior))
+        acc = CountedAccepter(StandardRWAccepter(pot, prior))
+        s = MCMCSampler(prop, acc, PhiloxRNG(seed), chain_offset=chain)
+        out = s.run(np.zeros(4), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+        assert np.array_equal(out, golden[f"rw_{kind}_samples"][chain])
+        assert acc.accepts == int(golden[f"rw_{kind}_counts"][chain, 1])

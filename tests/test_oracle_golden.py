@@ -108,6 +108,53 @@ def test_linear_chain_matches_reference_sampler(orc, golden):
     np.testing.assert_array_equal(samples, golden["lin_samples"])
 
 
+def _rw_schedule(kind, meta, i0, n):
+    """Step sizes of the reference's RW proposers for proposals i0+1 .. i0+n."""
+    delta_c, d_s, d_e, l = meta[5], meta[6], meta[7], meta[8]
+    if kind == "const":
+        return None, float(np.sqrt(2 * delta_c))
+    slope = (d_s - d_e) / l
+    d = [d_e if i > l else d_s - slope * i for i in range(i0 + 1, i0 + n + 1)]
+    sched = np.stack([np.sqrt(2) * np.sqrt(np.array(d)), np.ones(n)], axis=1)
+    return sched, 0.0
+
+
+@pytest.mark.parametrize("kind", ["const", "var"])
+def test_rw_chain_matches_reference_sampler(orc, golden, kind):
+    """ConstStep/VarStepStandardRWProposer + StandardRWAccepter (accepter.py:86-106,
+    incl. its sqrt-covariance regularizer, Q6) through the reference sampler vs the oracle."""
+    meta = golden["rw_meta"]
+    gamma, seed, n_samples, burn_in, interval = meta[0], int(meta[1]), int(meta[2]), int(meta[3]), int(meta[4])
+    op = LinearOperator(golden["rw_g"], arith="reference")
+    sq = np.sqrt(golden["rw_prior_var"])
+    y, ginv = golden["rw_y"], np.array([1 / gamma])
+    U = np.zeros((3, 4))
+    phi = orc.init_phi(op, U, y, ginv, reg_scale=sq)
+    acc = np.zeros(3, dtype=np.int64)
+    step = 0
+    samples = np.zeros((3, n_samples, 4))
+    blocks = [max(0, burn_in - interval)] + [interval] * n_samples
+    for b, n in enumerate(blocks):
+        sched, beta = _rw_schedule(kind, meta, step, n)
+        orc.pcn_sweep(op, U, phi, y, ginv, sq, beta, seed, step, n, accepts=acc, beta_schedule=sched,
+                      proposal="rw", reg_scale=sq)
+        step += n
+        if b > 0:
+            samples[:, b - 1] = U
+    assert np.array_equal(acc, golden[f"rw_{kind}_counts"][:, 1])
+    np.testing.assert_array_equal(samples, golden[f"rw_{kind}_samples"])
+
+
+def test_rw_accept_potential_matches_reference(orc, golden):
+    """I(u) = Φ(u) + ½‖C^{1/2}u‖² (accepter.py:104-106) vs StandardRWAccepter._I, up to Φ's constant."""
+    gamma = golden["rw_meta"][0]
+    op = LinearOperator(golden["rw_g"], arith="reference")
+    U = np.ascontiguousarray(golden["rw_I_u"])
+    got = orc.init_phi(op, U, golden["rw_y"], [1 / gamma], reg_scale=np.sqrt(golden["rw_prior_var"]))
+    const = 0.5 * (np.log(2 * np.pi) + np.log(gamma**2))
+    np.testing.assert_allclose(got + const, golden["rw_I"], rtol=1e-13, atol=1e-12)
+
+
 def test_linear_potential_matches_reference_up_to_constant(orc, golden):
     gamma = golden["lin_meta"][0]
     op = LinearOperator(golden["lin_g"], arith="reference")
