@@ -160,6 +160,13 @@ int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t 
 int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out,
                  void* stream);
 
+/* Batched normalised autocorrelation (MCMCSampler.autocorr, sampler.py:43-54):
+   series s is x[s*stride_series + t*stride_t], t < len (len <= 8192);
+   out[s, tau] = r[tau]/r[0], r[tau] = Σ_t x_[t] x_[t+tau], x_ = x - mean(x), tau < max_lag <= len;
+   all ones for a constant series.  out is double [n_series, max_lag]. */
+int ipmc_autocorr(const void* x, int32_t dtype, int64_t n_series, int64_t len, int64_t stride_series,
+                  int64_t stride_t, int32_t max_lag, double* out, void* stream);
+
 /* Layout the sweep kernel would use for this model/dtype when lanes_per_chain = chains_per_lane = 0:
    returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout. */
 int ipmc_auto_lanes(const ipmc_model* model, int32_t dtype, int64_t n_chains);

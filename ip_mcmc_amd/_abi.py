@@ -96,6 +96,10 @@ SIGNATURES = {
         [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p],
     ),
     "ipmc_uniform": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "ipmc_autocorr": (
+        C.c_int,
+        [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p],
+    ),
     "ipmc_auto_lanes": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_auto_layout": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_last_error": (C.c_char_p, []),

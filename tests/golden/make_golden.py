@@ -365,6 +365,11 @@ def make_misc(out):
             smp.run(np.array([1.0]), n_samples=n, burn_in=b, sample_interval=s)
         rows.append([b, n, s, a.calls])
     out["schedule"] = np.array(rows)
+    # MCMCSampler.autocorr (sampler.py:43-54) on random-walk series and a constant one
+    xs = np.random.default_rng(11).normal(size=(6, 120)).cumsum(axis=1)
+    xs[5] = 3.0
+    out["ac_x"] = xs
+    out["ac_ref"] = np.stack([MCMCSampler.autocorr(x) for x in xs])
 
 
 def main():
