@@ -33,6 +33,7 @@ from ._lib import UnsupportedOnDevice, call
 from .accepter import BoxConstraint, ConstrainAccepter, CountedAccepter, StandardRWAccepter, pCNAccepter
 from .distribution import GaussianDistribution
 from .potential import EvolutionPotential
+from .chainio import ChainState, NpySampleSink
 from .rng import PhiloxRNG, resolve_rng
 
 # pCN steps per chain in one kernel launch (launches are split at sample
@@ -122,18 +123,31 @@ class MCMCSampler:
         self.last_run_seconds = None
 
     # ------------------------------------------------------------------ run
-    def run(self, u_0, n_samples, burn_in=1000, sample_interval=200, keep="samples"):
+    def run(self, u_0, n_samples, burn_in=1000, sample_interval=200, keep="samples", sample_file=None,
+            flush_every=None):
         """Run the chain(s).  keep='samples' returns the samples like the
         reference; keep='moments' returns a dict of per-chain sums of u and u²
         over every post-burn-in step (no sample array); keep='last' returns
-        the final states (C, k)."""
+        the final states (C, k).
+
+        u_0 may be a ChainState (``checkpoint()`` / ``chainio.load_state``):
+        the run then continues those chains exactly (same Φ cache, Philox
+        position and proposer counter).  sample_file='x.npy' streams the
+        samples into a np.load-compatible file block by block (every
+        ``flush_every`` samples) and returns it memory-mapped."""
         if keep not in ("samples", "moments", "last"):
             raise ValueError("keep must be 'samples', 'moments' or 'last'")
         plan = _Plan(self.proposer, self.accepter)
         device = dev.resolve_device(self.device)
         td = dev.torch_dtype(self.dtype)
         k = plan.G.k
-        if isinstance(u_0, torch.Tensor):
+        resume = isinstance(u_0, ChainState)
+        if resume:
+            if u_0.u.shape[1] != k:
+                raise ValueError(f"ChainState has k={u_0.u.shape[1]}, forward map k={k}")
+            single = False
+            U = dev.to_device(u_0.u, td, device).clone()
+        elif isinstance(u_0, torch.Tensor):
             single = u_0.dim() <= 1
             U = u_0.reshape(-1, k).to(device=device, dtype=td).clone().contiguous()
         else:
@@ -146,7 +160,13 @@ class MCMCSampler:
         if n_samples < 0 or sample_interval < 0:
             raise ValueError("n_samples and sample_interval must be >= 0")
 
-        rng = resolve_rng(self.rng)
+        if resume:
+            rng = self.rng if isinstance(self.rng, PhiloxRNG) else PhiloxRNG()
+            rng.seed, rng.step = u_0.seed, u_0.step
+            if hasattr(plan.proposer, "i"):
+                plan.proposer.i = u_0.proposer_i
+        else:
+            rng = resolve_rng(self.rng)
         if isinstance(self.accepter, CountedAccepter):
             self.accepter.reset()  # sampler.py:15-16
 
@@ -188,7 +208,12 @@ class MCMCSampler:
             sw.beta, sw.contraction = plan.proposer.device_step()
         sw.seed = rng.seed
         # the accept potential of the starting states: Φ(u), or I(u) for StandardRWAccepter
-        call("ipmc_init_phi", C.byref(model), C.byref(sw), stream)
+        if resume:
+            if u_0.phi.shape[0] != n_chains:
+                raise ValueError("ChainState phi does not match its u")
+            phi.copy_(dev.to_device(u_0.phi, td, device))
+        else:
+            call("ipmc_init_phi", C.byref(model), C.byref(sw), stream)
 
         step = rng.step
         prop_i = getattr(plan.proposer, "i", 0)
@@ -224,8 +249,15 @@ class MCMCSampler:
 
         samples = None
         sums = None
+        sink = None
+        buf_len = n_samples
         if keep == "samples":
-            samples = torch.empty((n_chains, n_samples, k), dtype=td, device=device)
+            if sample_file is not None:
+                sink = NpySampleSink(sample_file, (n_samples, k) if single else (n_chains, n_samples, k))
+                # device staging buffer of <= ~256 MiB between flushes
+                auto = max(1, (1 << 28) // max(1, n_chains * k * 8))
+                buf_len = max(1, min(n_samples, int(flush_every) if flush_every else auto))
+            samples = torch.empty((n_chains, buf_len, k), dtype=td, device=device)
         elif keep == "moments":
             sums = (
                 torch.zeros((n_chains, k), dtype=torch.float64, device=device),
@@ -234,15 +266,19 @@ class MCMCSampler:
         for i in range(n_samples):  # sampler.py:23-28
             if self.verbose:
                 print(f"Sampling {i + 1}/{n_samples}")
+            slot = i % buf_len
             done = 0
             while done < sample_interval:
                 n = min(STEPS_PER_LAUNCH, sample_interval - done)
                 last = done + n == sample_interval
-                view = samples[:, i, :] if (samples is not None and last) else None
+                view = samples[:, slot, :] if (samples is not None and last) else None
                 launch(n, view, sums)
                 done += n
             if sample_interval == 0 and samples is not None:
-                launch(0, samples[:, i, :])
+                launch(0, samples[:, slot, :])
+            if sink is not None and (slot == buf_len - 1 or i == n_samples - 1):
+                blk = samples[:, : slot + 1, :].double().cpu().numpy()
+                sink.write(i - slot, blk[0] if single else blk)
         torch.cuda.synchronize(device)
         self.last_run_seconds = time.perf_counter() - t0
 
@@ -260,8 +296,17 @@ class MCMCSampler:
         if self.verbose and isinstance(self.accepter, CountedAccepter):
             print(f"Acceptance ratio: {self.accepter.ratio()}")  # sampler.py:30-31
 
-        self.state = {"u": U, "phi": phi, "accepts": accepts, "calls": calls, "steps": total, "rng": rng}
+        prev_acc = u_0.accepts if resume else 0
+        prev_calls = u_0.calls if (resume and u_0.calls is not None) else 0
+        self.state = ChainState(
+            U.cpu().numpy(), phi.cpu().numpy(), prev_acc + acc_np,
+            None if calls_np is None else prev_calls + calls_np, rng.seed, rng.step, prop_i,
+            "float64" if td == torch.float64 else "float32",
+        )
+        self.state.steps_this_run = total
         if keep == "samples":
+            if sink is not None:
+                return sink.close()
             out = samples.double().cpu().numpy()
             return out[0] if single else out
         if keep == "moments":
@@ -272,6 +317,13 @@ class MCMCSampler:
             return res
         last = U.double().cpu().numpy()
         return last[0] if single else last
+
+    def checkpoint(self):
+        """ChainState of the last run (save with chainio.save_state; pass it as
+        run()'s u_0 to continue the chains exactly)."""
+        if self.state is None:
+            raise ValueError("No run yet!")
+        return self.state
 
     def _step(self, u, rng):
         """sampler.py:35-41, one host step (API compatibility; not the hot path)."""
