@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 3
+#define IPMC_ABI_VERSION 4
 
 typedef enum {
   IPMC_OK = 0,
@@ -60,7 +60,9 @@ typedef enum {
   IPMC_MODEL_LINEAR = 0,    /* G(u) = A (theta0 + u)                  stuart_examples.py:69-70 */
   IPMC_MODEL_LORENZ63 = 1,  /* RK4 Lorenz-63, moments time-averaged   (no reference; lorenz_mcmc.py:17-40 pattern) */
   IPMC_MODEL_LORENZ96 = 2,  /* RK4 single-scale Lorenz-96, forcing field theta0+u, time-averaged X   lorenz.py:73-88 */
-  IPMC_MODEL_BURGERS = 3    /* Rusanov FV + SSPRK2 Burgers, windowed trapz observations   burgers/rusanov.py, utilities.py */
+  IPMC_MODEL_BURGERS = 3,   /* Rusanov FV + SSPRK2 Burgers, windowed trapz observations   burgers/rusanov.py, utilities.py */
+  IPMC_MODEL_LORENZ96_2S = 4 /* RK4 two-scale Lorenz-96 (lorenz.py:44-101), theta = (F, h, b), time-averaged
+                                5K moments (lorenz_mcmc.py:17-40, 55-68) */
 } ipmc_model_kind;
 
 typedef enum {
@@ -97,6 +99,10 @@ typedef struct ipmc_model {
   double meas_dx;     /* trapz spacing x[2]-x[1] of the interior centres (utilities.py:91) */
   int32_t max_iter;   /* CFL mode: step cap; a chain that hits it is invalid (Φ = +inf) */
   int32_t reserved;
+  /* Two-scale Lorenz-96 (IPMC_MODEL_LORENZ96_2S): dim = K slow variables, state K(1+J) */
+  int32_t fast_per_slow; /* J (lorenz.py:21-22) */
+  int32_t moment_mode;   /* 0: the reference moment_function (Ybar_k = Y_{k,0}, lorenz_mcmc.py:32, Q8); 1: block mean */
+  double coupling_c;     /* c, time-scale ratio (lorenz.py:27-28), fixed; theta = (F, h, b) = theta0 + u */
 } ipmc_model;
 
 /* One launch of n_steps pCN steps for n_chains chains. */

@@ -31,6 +31,7 @@ from .forward import (
     Lorenz63Operator,
     Lorenz96Operator,
     ObservationOperator,
+    TwoScaleLorenz96Operator,
 )
 from .rng import PhiloxRNG
 from ._lib import IpmcError, UnsupportedOnDevice
@@ -59,6 +60,7 @@ __all__ = [
     "Lorenz63Operator",
     "Lorenz96Operator",
     "ObservationOperator",
+    "TwoScaleLorenz96Operator",
     "PhiloxRNG",
     "IpmcError",
     "UnsupportedOnDevice",

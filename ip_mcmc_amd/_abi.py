@@ -4,11 +4,11 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
-MODEL_LINEAR, MODEL_LORENZ63, MODEL_LORENZ96, MODEL_BURGERS = 0, 1, 2, 3
+MODEL_LINEAR, MODEL_LORENZ63, MODEL_LORENZ96, MODEL_BURGERS, MODEL_LORENZ96_2S = 0, 1, 2, 3, 4
 ARITH_FMA, ARITH_REFERENCE = 0, 1
 DT_FIXED, DT_CFL = 0, 1
 PROPOSAL_PCN, PROPOSAL_RW = 0, 1
@@ -45,6 +45,9 @@ class IpmcModel(C.Structure):
         ("meas_dx", C.c_double),
         ("max_iter", C.c_int32),
         ("reserved", C.c_int32),
+        ("fast_per_slow", C.c_int32),
+        ("moment_mode", C.c_int32),
+        ("coupling_c", C.c_double),
     ]
 
 

@@ -50,6 +50,12 @@ static int check_model(const ipmc_model* m) {
       if (m->dim != m->k || m->q != m->dim) return fail(IPMC_ERR_INVALID, "Lorenz-96: k and q must equal dim");
       if (!m->x0 || m->n_steps <= 0) return fail(IPMC_ERR_INVALID, "Lorenz-96: x0 / n_steps");
       return IPMC_OK;
+    case IPMC_MODEL_LORENZ96_2S:
+      if (m->k != 3 || m->dim <= 0 || m->fast_per_slow <= 0 || m->q != 5 * m->dim)
+        return fail(IPMC_ERR_INVALID, "two-scale Lorenz-96: k must be 3, K, J > 0 and q == 5K");
+      if (!m->x0 || m->n_steps <= 0) return fail(IPMC_ERR_INVALID, "two-scale Lorenz-96: x0 / n_steps");
+      if (m->dim > 64) return fail(IPMC_ERR_UNSUPPORTED, "two-scale Lorenz-96: K <= 64");
+      return IPMC_OK;
     case IPMC_MODEL_BURGERS:
       if (m->k != 3 || m->q != m->n_windows || !m->win_lo || !m->win_hi || !m->x0 || m->dim < 2)
         return fail(IPMC_ERR_INVALID, "Burgers: k must be 3, q == n_windows, windows/centres set");
@@ -182,6 +188,8 @@ static int dispatch_eval(const ipmc_model* m, int32_t dtype, int64_t n, const vo
     }
     case IPMC_MODEL_BURGERS:
       return burgers_eval(*m, dtype, n, u, y, ginv, out, phi, st);
+    case IPMC_MODEL_LORENZ96_2S:
+      return l96ts_eval(*m, dtype, n, u, y, ginv, out, phi, st);
   }
   return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
 }
@@ -255,6 +263,8 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
     }
     case IPMC_MODEL_BURGERS:
       return burgers_sweep(*m, *s, st);
+    case IPMC_MODEL_LORENZ96_2S:
+      return l96ts_sweep(*m, *s, st);
   }
   return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
 }

@@ -26,4 +26,9 @@ int burgers_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st);
 int burgers_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
                  void* out, bool phi, hipStream_t st);
 
+// Two-scale Lorenz-96 with the moment observation (ipmc_l96ts.hip)
+int l96ts_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st);
+int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
+               void* out, bool phi, hipStream_t st);
+
 }  // namespace ipmc

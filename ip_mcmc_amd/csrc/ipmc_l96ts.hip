@@ -1,0 +1,319 @@
+// Two-scale Lorenz-96 (lorenz.py:44-101 with J > 0) forward map, observed by
+// the time-averaged moment function of lorenz_mcmc.py:17-40, and its pCN sweep.
+//
+// Layout: one chain per group of GS lanes (GS = the power of two >= K, <= 64);
+// lane k < K owns the slow variable X_k and its fast block Y_{k,0..J-1} in
+// VGPRs (1+J values per RK4 array).  The fast blocks are cyclic inside the
+// block (np.roll of Y_in[k, :]) so they never leave the lane; the slow
+// neighbours X_{k-2}, X_{k-1}, X_{k+1} (cyclic mod K) come by ds_bpermute.
+// theta = (F, h, b) = theta0 + u is the same on every lane of the group.
+// Lane k accumulates the five moments of slot k; Φ sums the 5K residuals in
+// observation order (every lane gathers them, so all lanes hold Φ).
+#include "ipmc_internal.hpp"
+#include "ipmc_sweep_common.hpp"
+
+namespace ipmc {
+
+constexpr int kTsBlock = 256;
+
+struct TsCtx {
+  int K, GS, sub, base;  // base = first lane of the group
+};
+
+// numpy pairwise_sum order (n <= 128) of a compile-time-sized array.
+template <typename T, int J>
+__device__ __forceinline__ T np_pairwise(const T (&a)[J], int off) {
+  if constexpr (J < 8) {
+    T res = (T)0;
+#pragma unroll
+    for (int i = 0; i < J; ++i) res = res + a[off + i];
+    return res;
+  } else {
+    T r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[off + j];
+    constexpr int full = J - (J % 8);
+#pragma unroll
+    for (int i = 8; i < full; i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + a[off + i + j];
+    }
+    T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int i = full; i < J; ++i) res = res + a[off + i];
+    return res;
+  }
+}
+
+// state s[0] = X_k, s[1 + j] = Y_{k,j}
+template <typename T, int J>
+__device__ __forceinline__ T block_mean(const T (&s)[1 + J]) {
+  T y[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) y[j] = s[1 + j];
+  return np_pairwise<T, J>(y, 0) / (T)J;
+}
+
+template <typename T, int J, bool FM>
+__device__ __forceinline__ void ts_rhs(const T (&s)[1 + J], T F, T hc, T hJ, T bb, T cc, const TsCtx& c,
+                                       T (&o)[1 + J]) {
+  const int K = c.K;
+  const T X = s[0];
+  const T xm1 = __shfl(X, c.base + (c.sub + K - 1) % K, 64);
+  const T xm2 = __shfl(X, c.base + (c.sub + K - 2) % K, 64);
+  const T xp1 = __shfl(X, c.base + (c.sub + 1) % K, 64);
+  const T yb = block_mean<T, J>(s);
+  if constexpr (FM) {
+    const T t = madd<true>(xp1 - xm2, xm1, F - X);
+    o[0] = madd<true>(-hc, yb, t);
+  } else {
+    T t = -X;
+    t = t - (xm1 * xm2 - xm1 * xp1);
+    t = t + F;
+    o[0] = t - hc * yb;
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const T y = s[1 + j];
+    const T yp1 = s[1 + (j + 1) % J], yp2 = s[1 + (j + 2) % J], ym1 = s[1 + (j + J - 1) % J];
+    T t;
+    if constexpr (FM) {
+      const T nl = yp1 * (yp2 - ym1);
+      t = madd<true>(hJ, X, -y);
+      t = madd<true>(-bb, nl, t);
+    } else {
+      t = -y;
+      t = t - bb * (yp1 * yp2 - ym1 * yp1);
+      t = t + hJ * X;
+    }
+    o[1 + j] = t * cc;
+  }
+}
+
+// Φ(theta0 + v) for the group; g_out (per chain, [5K]) receives G if set.
+template <typename T, int J, bool FM>
+__device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, const T* __restrict__ y,
+                    const T* __restrict__ ginv, T* g_out) {
+  const int K = c.K;
+  const bool live = c.sub < K;
+  const int k = live ? c.sub : 0;
+  const T* th0 = (const T*)m.theta0;
+  const T F = th0[0] + v[0], h = th0[1] + v[1], bb = th0[2] + v[2];
+  const T cc = (T)m.coupling_c;
+  const T hc = h * cc, hJ = h / (T)J;
+  const T hh = (T)m.dt, h2 = hh * (T)0.5, h6 = hh / (T)6;
+  const T* x0 = (const T*)m.x0;
+  T x[1 + J];
+  x[0] = x0[k];
+#pragma unroll
+  for (int j = 0; j < J; ++j) x[1 + j] = x0[K + k * J + j];
+  T ob[5] = {0, 0, 0, 0, 0};
+  const bool refmom = (m.moment_mode == 0);
+  for (int n = 0; n < m.n_steps; ++n) {
+    T k1[1 + J], acc[1 + J], xs[1 + J];
+    ts_rhs<T, J, FM>(x, F, hc, hJ, bb, cc, c, k1);
+#pragma unroll
+    for (int i = 0; i <= J; ++i) {
+      acc[i] = k1[i];
+      xs[i] = madd<FM>(h2, k1[i], x[i]);
+    }
+    ts_rhs<T, J, FM>(xs, F, hc, hJ, bb, cc, c, k1);
+#pragma unroll
+    for (int i = 0; i <= J; ++i) {
+      acc[i] = madd<FM>((T)2, k1[i], acc[i]);
+      xs[i] = madd<FM>(h2, k1[i], x[i]);
+    }
+    ts_rhs<T, J, FM>(xs, F, hc, hJ, bb, cc, c, k1);
+#pragma unroll
+    for (int i = 0; i <= J; ++i) {
+      acc[i] = madd<FM>((T)2, k1[i], acc[i]);
+      xs[i] = madd<FM>(hh, k1[i], x[i]);
+    }
+    ts_rhs<T, J, FM>(xs, F, hc, hJ, bb, cc, c, k1);
+#pragma unroll
+    for (int i = 0; i <= J; ++i) {
+      acc[i] = acc[i] + k1[i];
+      x[i] = madd<FM>(h6, acc[i], x[i]);
+    }
+    const T X = x[0];
+    const T yb = refmom ? x[1] : block_mean<T, J>(x);
+    ob[0] = ob[0] + X;
+    ob[1] = ob[1] + yb;
+    ob[2] = madd<FM>(X, X, ob[2]);
+    ob[3] = madd<FM>(X, yb, ob[3]);
+    ob[4] = madd<FM>(yb, yb, ob[4]);
+  }
+  const T nn = (T)m.n_steps;
+  T r[5];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    const T g = ob[b] / nn;
+    if (g_out && live) g_out[b * K + k] = g;
+    r[b] = y ? (y[b * K + k] - g) * ginv[b * K + k] : (T)0;
+  }
+  T s = (T)0;
+  if (y) {
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      for (int kk = 0; kk < K; ++kk) {
+        const T val = __shfl(r[b], c.base + kk, 64);
+        s = madd<FM>(val, val, s);
+      }
+    }
+  }
+  return (T)0.5 * s;
+}
+
+template <typename T, int J, bool FM>
+__global__ __launch_bounds__(kTsBlock) void l96ts_sweep_kernel(const ipmc_model m, const ipmc_sweep s, int GS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * kTsBlock + threadIdx.x;
+  const int64_t chain = tid / GS;
+  const TsCtx c{m.dim, GS, (int)(tid % GS), lane & ~(GS - 1)};
+  if (chain >= s.n_chains) return;
+  const uint64_t gid = (uint64_t)(s.chain_offset + chain);
+  T* u = (T*)s.u + chain * 3;
+  T ur[3] = {u[0], u[1], u[2]};
+  const T* sq = (const T*)s.prior_sqrt;
+  const T beta = (T)s.beta, contr = (T)s.contraction;
+  const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
+  T* phi = (T*)s.phi;
+  T phu = phi[chain];
+  int64_t nacc = 0, ncalls = 0;
+  for (int64_t st = 0; st < s.n_steps; ++st) {
+    const uint64_t step = s.step0 + (uint64_t)st;
+    const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
+    const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
+    T v[3];
+    pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw);
+    bool ok = true;
+    if (s.box_lo || s.box_hi) {
+      const T* lo = (const T*)s.box_lo;
+      const T* hi = (const T*)s.box_hi;
+      const T* off = (const T*)s.box_off;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const T t = v[j] + (off ? off[j] : (T)0);
+        if (lo && !(lo[j] < t)) ok = false;
+        if (hi && !(t < hi[j])) ok = false;
+      }
+    }
+    if (ok) {
+      ++ncalls;
+      T phv = ts_phi<T, J, FM>(m, v, c, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
+      if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
+      if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) ur[j] = v[j];
+        phu = phv;
+        ++nacc;
+      }
+    }
+    if (s.sum_u && c.sub == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double ud = (double)ur[j];
+        s.sum_u[chain * 3 + j] += ud;
+        if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+      }
+    }
+  }
+  if (c.sub == 0) {
+    phi[chain] = phu;
+    if (s.accepts) s.accepts[chain] += nacc;
+    if (s.calls) s.calls[chain] += ncalls;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) u[j] = ur[j];
+    if (s.sample_out) {
+      T* so = (T*)s.sample_out + chain * s.sample_stride;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) so[j] = ur[j];
+    }
+  }
+}
+
+template <typename T, int J, bool FM, bool PHI>
+__global__ __launch_bounds__(kTsBlock) void l96ts_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
+                                                              const T* __restrict__ y, const T* __restrict__ ginv,
+                                                              T* __restrict__ out, int GS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tid = (int64_t)blockIdx.x * kTsBlock + threadIdx.x;
+  const int64_t chain = tid / GS;
+  const TsCtx c{m.dim, GS, (int)(tid % GS), lane & ~(GS - 1)};
+  if (chain >= n) return;
+  const T v[3] = {uin[chain * 3], uin[chain * 3 + 1], uin[chain * 3 + 2]};
+  const T ph = ts_phi<T, J, FM>(m, v, c, PHI ? y : nullptr, ginv, PHI ? nullptr : out + chain * m.q);
+  if (PHI && c.sub == 0) out[chain] = ph;
+}
+
+static int group_size(int K) {
+  int g = 1;
+  while (g < K) g <<= 1;
+  return g;
+}
+
+#define IPMC_TS_J(X) X(1) X(2) X(4) X(8) X(10) X(16)
+
+template <typename T, bool FM>
+static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  const int GS = group_size(m.dim);
+  const int64_t blocks = (s.n_chains * GS + kTsBlock - 1) / kTsBlock;
+  switch (m.fast_per_slow) {
+#define IPMC_J(J)                                                                                             \
+  case J:                                                                                                     \
+    hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, GS); \
+    return check_launch("l96ts_sweep_kernel");
+    IPMC_TS_J(IPMC_J)
+#undef IPMC_J
+  }
+  set_error("two-scale Lorenz-96: no kernel compiled for J=%d (1, 2, 4, 8, 10, 16)", m.fast_per_slow);
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+template <typename T, bool FM>
+static int ts_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
+                     bool phi, hipStream_t st) {
+  const int GS = group_size(m.dim);
+  const int64_t blocks = (n * GS + kTsBlock - 1) / kTsBlock;
+  switch (m.fast_per_slow) {
+#define IPMC_J(J)                                                                                             \
+  case J:                                                                                                     \
+    if (phi)                                                                                                  \
+      hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, true>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, \
+                         n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out, GS);                           \
+    else                                                                                                      \
+      hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, false>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st,   \
+                         m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out, GS);                        \
+    return check_launch("l96ts_eval_kernel");
+    IPMC_TS_J(IPMC_J)
+#undef IPMC_J
+  }
+  set_error("two-scale Lorenz-96: no kernel compiled for J=%d (1, 2, 4, 8, 10, 16)", m.fast_per_slow);
+  return IPMC_ERR_UNSUPPORTED;
+}
+
+int l96ts_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+  if (m.dim > 64) {
+    set_error("two-scale Lorenz-96: K <= 64");
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true>(m, s, st) : ts_sweep_t<double, false>(m, s, st);
+  return fm ? ts_sweep_t<float, true>(m, s, st) : ts_sweep_t<float, false>(m, s, st);
+}
+
+int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
+               void* out, bool phi, hipStream_t st) {
+  if (m.dim > 64) {
+    set_error("two-scale Lorenz-96: K <= 64");
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (dtype == IPMC_F64)
+    return fm ? ts_eval_t<double, true>(m, n, u, y, ginv, out, phi, st)
+              : ts_eval_t<double, false>(m, n, u, y, ginv, out, phi, st);
+  return fm ? ts_eval_t<float, true>(m, n, u, y, ginv, out, phi, st)
+            : ts_eval_t<float, false>(m, n, u, y, ginv, out, phi, st);
+}
+
+}  // namespace ipmc

@@ -11,6 +11,7 @@ same description to the fused sweep kernel, so G never leaves the device.
   LinearOperator     G(u) = A (theta0 + u)                       stuart_examples.py:69-70
   Lorenz63Operator   RK4 Lorenz-63, moments time-averaged        (no reference; SURVEY §8(d) cfg 2)
   Lorenz96Operator   RK4 single-scale Lorenz-96 forcing field     lorenz.py:73-88, lorenz_mcmc.py:55-68
+  TwoScaleLorenz96Operator  RK4 two-scale L96, 5K moments         lorenz.py:44-101, lorenz_mcmc.py:17-71
   BurgersOperator    Rusanov FV + SSPRK2, windowed trapz          burgers/rusanov.py:6-109, utilities.py:17-109
 
 Every operator takes ``arith='fma'`` (default, fused multiply-adds) or
@@ -207,6 +208,81 @@ class Lorenz96Operator(ObservationOperator):
             k2 = cls.rhs(x + 0.5 * dt * k1, F)
             k3 = cls.rhs(x + 0.5 * dt * k2, F)
             k4 = cls.rhs(x + dt * k3, F)
+            x = x + dt / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
+        return x
+
+
+class TwoScaleLorenz96Operator(ObservationOperator):
+    """Two-scale Lorenz-96 (lorenz.py:44-101, K slow X_k each coupled to J fast
+    Y_{k,j}) observed by the time-averaged moment function of
+    lorenz_mcmc.py:17-40: G = time averages over the n post-step RK4 states of
+    [X, Ȳ, X², XȲ, Ȳ²] (q = 5K).  theta = (F, h, b) = prior_means + u
+    (lorenz_mcmc.py:64), c fixed (lorenz_mcmc.py:121).
+
+    moments='reference' takes Ȳ_k = Y_{k,0} as the reference does
+    (lorenz_mcmc.py:32, np.mean of one element); moments='mean'
+    takes the block mean over j.  State order as the reference's:
+    [X_0..X_{K-1}, Y_{0,0}..Y_{0,J-1}, Y_{1,0}, ...].  Stateless like
+    Lorenz96Operator: every evaluation starts from x0.
+    Classical RK4 replaces solve_ivp's RK45."""
+
+    kind = _abi.MODEL_LORENZ96_2S
+    J_COMPILED = (1, 2, 4, 8, 10, 16)
+
+    def __init__(self, K=6, J=4, prior_means=(12.0, 8.0, 9.0), c=1.0, x0=None, dt=0.005, n_steps=4000,
+                 moments="reference", arith="fma"):
+        super().__init__(arith)
+        self.K, self.J = int(K), int(J)
+        if not 1 <= self.K <= 64:
+            raise ValueError("TwoScaleLorenz96Operator: 1 <= K <= 64 on the device")
+        if self.J not in self.J_COMPILED:
+            raise ValueError(f"TwoScaleLorenz96Operator: J must be one of {self.J_COMPILED}")
+        if moments not in ("reference", "mean"):
+            raise ValueError("moments must be 'reference' or 'mean'")
+        self.moments = moments
+        self.k, self.q = 3, 5 * self.K
+        self.theta0 = np.asarray(prior_means, dtype=np.float64).reshape(3)
+        self.c = float(c)
+        if x0 is None:
+            x0 = self.spinup(self.K, self.J, (10.0, 10.0, self.c, 10.0), dt=dt, n_steps=2000)
+        self.x0 = np.asarray(x0, dtype=np.float64).reshape(self.K * (1 + self.J))
+        self.dt = float(dt)
+        self.n_steps = int(n_steps)
+
+    def _spec(self):
+        return (
+            {
+                "dim": self.K,
+                "fast_per_slow": self.J,
+                "moment_mode": 0 if self.moments == "reference" else 1,
+                "coupling_c": self.c,
+                "n_steps": self.n_steps,
+                "dt": self.dt,
+            },
+            {"theta0": self.theta0, "x0": self.x0},
+            {},
+        )
+
+    @staticmethod
+    def rhs(x, K, J, F, h, c, b):
+        """d(state)/dt (host numpy, problem setup), lorenz.py:44-101."""
+        X, Y = x[:K], x[K:].reshape(K, J)
+        dX = -X - (np.roll(X, 1) * np.roll(X, 2) - np.roll(X, 1) * np.roll(X, -1)) + F - h * c * Y.mean(axis=1)
+        nl = np.roll(Y, -1, axis=1) * np.roll(Y, -2, axis=1) - np.roll(Y, 1, axis=1) * np.roll(Y, -1, axis=1)
+        dY = c * (-Y - b * nl + (h / J) * X[:, None])
+        return np.concatenate([dX, dY.reshape(-1)])
+
+    @classmethod
+    def spinup(cls, K, J, theta=(10.0, 10.0, 1.0, 10.0), dt=0.005, n_steps=2000, seed=1):
+        """RK4 spin-up on the host from default_rng(seed).random, as
+        lorenz_mcmc.py:76-79 seeds its truth run (theta = F, h, c, b)."""
+        F, h, c, b = theta
+        x = np.random.default_rng(seed).random((J + 1) * K)
+        for _ in range(n_steps):
+            k1 = cls.rhs(x, K, J, F, h, c, b)
+            k2 = cls.rhs(x + 0.5 * dt * k1, K, J, F, h, c, b)
+            k3 = cls.rhs(x + 0.5 * dt * k2, K, J, F, h, c, b)
+            k4 = cls.rhs(x + dt * k3, K, J, F, h, c, b)
             x = x + dt / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
         return x
 

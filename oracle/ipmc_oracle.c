@@ -48,6 +48,11 @@ static int check_model(const ipmc_model* m) {
     case IPMC_MODEL_LORENZ96:
       return (m->dim == m->k && m->q == m->dim && m->x0 && m->theta0 && m->n_steps > 0) ? IPMC_OK
                                                                                        : IPMC_ERR_INVALID;
+    case IPMC_MODEL_LORENZ96_2S:
+      return (m->k == 3 && m->dim > 0 && m->fast_per_slow > 0 && m->q == 5 * m->dim && m->x0 && m->theta0 &&
+              m->n_steps > 0)
+                 ? IPMC_OK
+                 : IPMC_ERR_INVALID;
     case IPMC_MODEL_BURGERS:
       return (m->k == 3 && m->q == m->n_windows && m->x0 && m->theta0 && m->win_lo && m->win_hi && m->dim > 1)
                  ? IPMC_OK
@@ -124,6 +129,12 @@ void orc_l96_rhs_f64(int32_t arith, int32_t d, const double* x, const double* F,
   l96_rhs_f64(arith == IPMC_ARITH_FMA, d, x, F, out);
 }
 
+/* Two-scale Lorenz-96 right-hand side (lorenz.py:44-101), fp64; p = (F, h, c, b). */
+void orc_l96ts_rhs_f64(int32_t arith, int32_t K, int32_t J, const double* x, const double* p, double* out) {
+  const double hc = p[1] * p[2], hJ = p[1] / (double)J;
+  l96ts_rhs_f64(arith == IPMC_ARITH_FMA, K, J, p[0], hc, hJ, p[3], p[2], x, out);
+}
+
 /* Rusanov pieces for the rusanov.py:112-170 known-answer tests. */
 double orc_rusanov_flux_f64(int32_t arith, double a, double b) {
   return rus_flux_f64(arith == IPMC_ARITH_FMA, a, b);
@@ -132,65 +143,5 @@ void orc_rusanov_rate_f64(int32_t arith, int32_t N, const double* w, double dx, 
   rus_rate_f64(arith == IPMC_ARITH_FMA, N, w, -dx, 0.0, 0, r);
 }
 
-
-/* Struct layout as this C compiler sees include/ipmc.h (checked by tests/test_lib_exports.py). */
-#include <stddef.h>
-int orc_layout(int64_t* out) {
-  int i = 0;
-  out[i++] = (int64_t)sizeof(ipmc_model);
-  out[i++] = (int64_t)offsetof(ipmc_model, kind);
-  out[i++] = (int64_t)offsetof(ipmc_model, arith);
-  out[i++] = (int64_t)offsetof(ipmc_model, k);
-  out[i++] = (int64_t)offsetof(ipmc_model, q);
-  out[i++] = (int64_t)offsetof(ipmc_model, dim);
-  out[i++] = (int64_t)offsetof(ipmc_model, n_steps);
-  out[i++] = (int64_t)offsetof(ipmc_model, dt);
-  out[i++] = (int64_t)offsetof(ipmc_model, x0);
-  out[i++] = (int64_t)offsetof(ipmc_model, theta0);
-  out[i++] = (int64_t)offsetof(ipmc_model, A);
-  out[i++] = (int64_t)offsetof(ipmc_model, dt_mode);
-  out[i++] = (int64_t)offsetof(ipmc_model, n_windows);
-  out[i++] = (int64_t)offsetof(ipmc_model, win_lo);
-  out[i++] = (int64_t)offsetof(ipmc_model, win_hi);
-  out[i++] = (int64_t)offsetof(ipmc_model, dx);
-  out[i++] = (int64_t)offsetof(ipmc_model, t_end);
-  out[i++] = (int64_t)offsetof(ipmc_model, cfl);
-  out[i++] = (int64_t)offsetof(ipmc_model, nu);
-  out[i++] = (int64_t)offsetof(ipmc_model, meas_scale);
-  out[i++] = (int64_t)offsetof(ipmc_model, meas_dx);
-  out[i++] = (int64_t)offsetof(ipmc_model, max_iter);
-  out[i++] = (int64_t)offsetof(ipmc_model, reserved);
-  out[i++] = (int64_t)sizeof(ipmc_sweep);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, dtype);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, lanes_per_chain);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, chains_per_lane);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, reserved0);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, n_chains);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, chain_offset);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, u);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, phi);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, accepts);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, calls);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, y);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, gamma_inv);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, prior_sqrt);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, box_lo);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, box_hi);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, box_off);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, beta);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, contraction);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, beta_schedule);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, proposal);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, reserved1);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, reg_scale);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, seed);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, step0);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, n_steps);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, sample_out);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, sample_stride);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, sum_u);
-  out[i++] = (int64_t)offsetof(ipmc_sweep, sum_u2);
-  return i;
-}
 
 int orc_abi_version(void) { return IPMC_ABI_VERSION; }

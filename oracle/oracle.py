@@ -45,6 +45,8 @@ def lib():
         h.orc_philox4x32_10.restype = None
         h.orc_l96_rhs_f64.argtypes = [C.c_int32, C.c_int32, P, P, P]
         h.orc_l96_rhs_f64.restype = None
+        h.orc_l96ts_rhs_f64.argtypes = [C.c_int32, C.c_int32, C.c_int32, P, P, P]
+        h.orc_l96ts_rhs_f64.restype = None
         h.orc_rusanov_flux_f64.argtypes = [C.c_int32, C.c_double, C.c_double]
         h.orc_rusanov_flux_f64.restype = C.c_double
         h.orc_rusanov_rate_f64.argtypes = [C.c_int32, C.c_int32, P, C.c_double, P]
@@ -222,6 +224,16 @@ def l96_rhs(x, F, arith="reference"):
     F = np.ascontiguousarray(np.broadcast_to(np.asarray(F, dtype=np.float64), x.shape))
     out = np.empty_like(x)
     lib().orc_l96_rhs_f64(_abi.ARITH_FMA if arith == "fma" else _abi.ARITH_REFERENCE, x.size, _p(x), _p(F), _p(out))
+    return out
+
+
+def l96ts_rhs(x, K, J, p, arith="reference"):
+    """Two-scale Lorenz-96 RHS, p = (F, h, c, b)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    p = np.ascontiguousarray(p, dtype=np.float64)
+    assert x.size == K * (1 + J) and p.size == 4
+    out = np.empty_like(x)
+    lib().orc_l96ts_rhs_f64(_abi.ARITH_FMA if arith == "fma" else _abi.ARITH_REFERENCE, K, J, _p(x), _p(p), _p(out))
     return out
 
 

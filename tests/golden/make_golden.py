@@ -53,6 +53,7 @@ from ip_mcmc import (  # noqa: E402
 
 ip_mcmc.pCNProposer = ConstSteppCNProposer  # stale name in lorenz.py:8
 import lorenz  # noqa: E402  report/scripts/lorenz.py
+import lorenz_mcmc  # noqa: E402  report/scripts/lorenz_mcmc.py (moment_function)
 import rusanov  # noqa: E402  report/scripts/burgers/rusanov.py
 
 from oracle import oracle as O  # noqa: E402  (draws only: Philox stream)
@@ -197,6 +198,73 @@ def make_l96_chain(out):
     out["l96c_meta"] = np.array([K, n, dt, gamma, 0.3, seed, 6, 20, 10], dtype=np.float64)
     out["l96c_samples"] = np.stack([c[0] for c in chains])
     out["l96c_decisions"] = np.stack([np.array(c[1]) for c in chains])
+
+
+# ------------------------------------------------- two-scale Lorenz-96
+def l96ts_G(K, J, theta, c, x0, dt, n):
+    """Two-scale G: RK4 (contract order, as rk4_time_average) with the
+    reference RHS object Lorenz96(K, J, F, h, c, b), the post-step states fed
+    to the reference moment_function (lorenz_mcmc.py:17-40), and its columns
+    time-averaged in step order (the build's accumulation contract)."""
+    F, h, b = theta
+    obj = lorenz.Lorenz96(K, J, F, h, c, b)
+    x = np.array(x0, dtype=np.float64)
+    hh, h2, h6 = dt, dt * 0.5, dt / 6.0
+    traj = np.empty((x.size, n))
+    for t in range(n):
+        k1 = obj(0.0, x)
+        k2 = obj(0.0, x + h2 * k1)
+        k3 = obj(0.0, x + h2 * k2)
+        k4 = obj(0.0, x + hh * k3)
+        x = x + h6 * (((k1 + 2.0 * k2) + 2.0 * k3) + k4)
+        traj[:, t] = x
+    f = lorenz_mcmc.moment_function(traj, K, J)
+    ob = np.zeros(5 * K)
+    for t in range(n):
+        ob = ob + f[:, t]
+    return ob / float(n)
+
+
+def make_l96ts(out):
+    rng = np.random.default_rng(4321)
+    # RHS of the reference object on random states, (K, J) incl. J = 1 and 16
+    for K, J in ((6, 4), (5, 8), (4, 10), (3, 1), (7, 16), (2, 2)):
+        n = 8
+        X = rng.normal(0, 3, size=(n, K * (1 + J)))
+        P = np.stack([rng.normal(10, 2, size=n), rng.normal(5, 2, size=n), rng.uniform(0.5, 10, size=n),
+                      rng.normal(8, 2, size=n)], axis=1)  # F, h, c, b
+        R = np.stack([lorenz.Lorenz96(K, J, *P[i])(0.0, X[i]) for i in range(n)])
+        out[f"ts_rhs_{K}_{J}_x"], out[f"ts_rhs_{K}_{J}_p"], out[f"ts_rhs_{K}_{J}_out"] = X, P, R
+    # moment_function on a random trajectory (reference, incl. its Ybar = Y_{k,0})
+    Y = rng.normal(0, 2, size=(6 * 5, 11))
+    out["ts_mom_y"], out["ts_mom_f"] = Y, lorenz_mcmc.moment_function(Y, 6, 4)
+    # G: K=6 J=4 (the thesis's problem), K=4 J=8, K=3 J=1
+    for K, J, n, dt in ((6, 4, 60, 0.005), (4, 8, 40, 0.004), (3, 1, 50, 0.01)):
+        x0 = rng.normal(0, 1, size=K * (1 + J))
+        th0 = np.array([12.0, 8.0, 9.0])
+        U = rng.normal(0, 0.5, size=(4, 3))
+        G = np.stack([l96ts_G(K, J, th0 + U[i], 1.0, x0, dt, n) for i in range(4)])
+        out[f"ts_G{K}_{J}_x0"], out[f"ts_G{K}_{J}_u"], out[f"ts_G{K}_{J}_G"] = x0, U, G
+        out[f"ts_G{K}_{J}_meta"] = np.array([n, dt, 1.0])
+    # pCN chains through the reference sampler, K=4 J=4
+    K, J, n, dt, c = 4, 4, 30, 0.005, 1.0
+    x0 = rng.normal(0, 1, size=K * (1 + J))
+    th0 = np.array([12.0, 8.0, 9.0])
+    y = l96ts_G(K, J, th0 + np.array([-1.0, 1.0, 0.5]), c, x0, dt, n) + 0.05 * rng.normal(size=5 * K)
+    gamma, beta, seed = 0.2, 0.4, 0x5EED2
+    chains = []
+    for chain in range(2):
+        def G(u):
+            return l96ts_G(K, J, th0 + u, c, x0, dt, n)
+
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, np.full(5 * K, gamma**2), np.array([10.0, 1.0, 10.0]), beta, np.zeros(3), seed, chain,
+            n_samples=4, burn_in=6, interval=3)
+        chains.append((s, dec))
+    out["tsc_x0"], out["tsc_y"] = x0, y
+    out["tsc_meta"] = np.array([K, J, n, dt, c, gamma, beta, seed, 4, 6, 3], dtype=np.float64)
+    out["tsc_samples"] = np.stack([ch[0] for ch in chains])
+    out["tsc_decisions"] = np.stack([np.array(ch[1]) for ch in chains])
 
 
 # -------------------------------------------------------- linear Gaussian
@@ -376,6 +444,7 @@ def main():
     out = {}
     make_l96(out)
     make_l96_chain(out)
+    make_l96ts(out)
     make_linear(out)
     make_rw(out)
     make_burgers(out)

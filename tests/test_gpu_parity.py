@@ -480,3 +480,85 @@ def test_sampler_rw_matches_reference_fixture(dev, golden, kind):
         out = s.run(np.zeros(4), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
         assert np.array_equal(out, golden[f"rw_{kind}_samples"][chain])
         assert acc.accepts == int(golden[f"rw_{kind}_counts"][chain, 1])
+
+
+# ------------------------------------------- two-scale Lorenz-96 (§8(f) #4)
+def _ts_ops():
+    from ip_mcmc_amd import TwoScaleLorenz96Operator as TS
+
+    rng = np.random.default_rng(21)
+    out = []
+    for arith in ("fma", "reference"):
+        for K, J, mom in ((6, 4, "reference"), (6, 4, "mean"), (4, 8, "mean"), (36, 10, "mean"), (3, 1, "reference"),
+                          (5, 16, "reference"), (40, 2, "mean"), (64, 1, "mean")):
+            x0 = rng.normal(0, 1, size=K * (1 + J))
+            out.append(TS(K=K, J=J, x0=x0, dt=0.004, n_steps=40, moments=mom, arith=arith))
+    return out
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_l96ts_forward_potential_bit_exact(dev, orc, dtype):
+    from ip_mcmc_amd import EvolutionPotential, GaussianDistribution
+
+    rng = np.random.default_rng(8)
+    for op in _ts_ops():
+        U = 0.3 * rng.normal(size=(67, 3))
+        g = op.forward_device(_t(U, dtype, dev)).cpu().numpy()
+        go = orc.forward(op, U, _np(dtype))
+        assert np.array_equal(g, go), (op.K, op.J, op.moments, op.arith, np.abs(g - go).max())
+        y = go[0] + 0.1 * rng.normal(size=op.q)
+        ginv = 1.0 / (0.1 + rng.random(op.q))
+        pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(op.q), np.diag(1 / ginv**2)))
+        phi = pot.phi_device(_t(U, dtype, dev)).cpu().numpy()
+        assert np.array_equal(phi, orc.potential(op, U, y, pot.device_terms()[1], _np(dtype))), (op.K, op.J)
+
+
+def test_l96ts_device_matches_reference_fixture(dev, golden):
+    from ip_mcmc_amd import TwoScaleLorenz96Operator as TS
+
+    for K, J in ((6, 4), (4, 8), (3, 1)):
+        n, dt, c = golden[f"ts_G{K}_{J}_meta"]
+        op = TS(K=K, J=J, c=c, x0=golden[f"ts_G{K}_{J}_x0"], dt=dt, n_steps=int(n), arith="reference")
+        g = op.forward_device(_t(golden[f"ts_G{K}_{J}_u"], torch.float64, dev)).cpu().numpy()
+        assert np.array_equal(g, golden[f"ts_G{K}_{J}_G"]), (K, J)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_l96ts_sweeps_bit_exact(dev, orc, dtype):
+    """pCN and RW (+ regularizer, schedule, box) sweeps of the two-scale model."""
+    ops = _ts_ops()
+    for op in (ops[0], ops[3], ops[12], ops[15]):
+        U0, phi0, y, ginv, sq = _problem(op, 77, dtype, orc, seed=op.K)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 9, 2, 5, dtype, dev, want_sums=True)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 9, 2, 5, dtype, want_sums=True)
+        _assert_same(d, o, (op.K, op.J, op.arith))
+        assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["samp"], o["u"])
+        box = (np.array([-np.inf, 7.8, -np.inf]), None, op.theta0)
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 9, 2, 5, dtype, dev, box=box)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 9, 2, 5, dtype, box=box)
+        _assert_same(d, o, (op.K, op.J, "box"))
+        assert o["calls"].sum() < 77 * 5, "box never rejected: vacuous"
+        rs = np.array([0.5, 1.0, 2.0])
+        phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
+        sched = np.stack([np.linspace(0.05, 0.2, 4), np.ones(4)], axis=1)
+        d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 5, 0, 4, dtype, dev, sched=sched, proposal="rw",
+                          reg_scale=rs)
+        o = _sweep_oracle(orc, op, U0, phr, y, ginv, sq, 0.1, 5, 0, 4, dtype, sched=sched, proposal="rw",
+                          reg_scale=rs)
+        _assert_same(d, o, (op.K, op.J, "rw"))
+
+
+def test_sampler_l96ts_chain_matches_reference_fixture(dev, golden):
+    """Reference sampler on the two-scale problem (injected draws) reproduced by MCMCSampler on the GPU."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, MCMCSampler, PhiloxRNG,
+                             TwoScaleLorenz96Operator, pCNAccepter)
+
+    K, J, n, dt, c, gamma, beta, seed, n_samples, burn_in, interval = golden["tsc_meta"]
+    op = TwoScaleLorenz96Operator(K=int(K), J=int(J), c=c, x0=golden["tsc_x0"], dt=dt, n_steps=int(n),
+                                  arith="reference")
+    q = op.q
+    pot = EvolutionPotential(op, golden["tsc_y"], GaussianDistribution(np.zeros(q), gamma**2 * np.eye(q)))
+    prior = GaussianDistribution(np.zeros(3), np.diag([10.0, 1.0, 10.0]))
+    s = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(int(seed)))
+    out = s.run(np.zeros((2, 3)), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+    assert np.array_equal(out, golden["tsc_samples"])

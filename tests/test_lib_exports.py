@@ -39,7 +39,7 @@ def test_struct_layout_matches_header():
 
 
 def test_oracle_library_loads(orc):
-    assert orc.lib().orc_abi_version() == 3
+    assert orc.lib().orc_abi_version() == 4
 
 
 def test_struct_offsets_match_c_compiler(orc):

@@ -6,7 +6,7 @@ from the reference itself (ochsnerd/ip_mcmc in /root/reference).
 import numpy as np
 import pytest
 
-from ip_mcmc_amd.forward import BurgersOperator, LinearOperator, Lorenz96Operator
+from ip_mcmc_amd.forward import BurgersOperator, LinearOperator, Lorenz96Operator, TwoScaleLorenz96Operator
 
 
 # ----------------------------------------------------------------- RNG
@@ -171,6 +171,63 @@ def test_l96_chain_matches_reference_sampler(orc, golden):
                            int(interval), 3, np.ones(K))
     assert np.array_equal(acc, golden["l96c_decisions"].sum(axis=1))
     np.testing.assert_array_equal(samples, golden["l96c_samples"])
+
+
+# ------------------------------------------------- two-scale Lorenz-96
+TS_RHS_CASES = [(6, 4), (5, 8), (4, 10), (3, 1), (7, 16), (2, 2)]
+
+
+@pytest.mark.parametrize("K,J", TS_RHS_CASES)
+def test_l96ts_rhs_reference_order_bit_exact(orc, golden, K, J):
+    """Two-scale Lorenz96.__call__ (lorenz.py:44-101) reproduced bit for bit (REFERENCE arith)."""
+    X, P, R = golden[f"ts_rhs_{K}_{J}_x"], golden[f"ts_rhs_{K}_{J}_p"], golden[f"ts_rhs_{K}_{J}_out"]
+    got = np.stack([orc.l96ts_rhs(X[i], K, J, P[i]) for i in range(len(X))])
+    assert np.array_equal(got, R)
+    fm = np.stack([orc.l96ts_rhs(X[i], K, J, P[i], "fma") for i in range(len(X))])
+    np.testing.assert_allclose(fm, R, rtol=1e-12, atol=1e-12 * np.abs(R).max())
+
+
+@pytest.mark.parametrize("name,K,J,p", [
+    ("forcing", 3, 1, (2, 1, 1, 1)),
+    ("slow_nonlinearity", 4, 1, (0, 0, 0, 0)),
+    ("fast_nonlinearity", 1, 4, (0, 0, 1, 2)),
+    ("step", 2, 2, (1, 1, 1, 1)),
+])
+def test_l96ts_reference_kats(orc, golden, name, K, J, p):
+    """All four test_Lorenz96 known answers (lorenz.py:114-171), two-scale RHS."""
+    x = golden[f"l96_kat_{name}_in"]
+    assert np.array_equal(orc.l96ts_rhs(x, K, J, p), golden[f"l96_kat_{name}_out"])
+
+
+@pytest.mark.parametrize("K,J", [(6, 4), (4, 8), (3, 1)])
+def test_l96ts_forward_reference_bit_exact(orc, golden, K, J):
+    """G = time-averaged reference moment_function (lorenz_mcmc.py:17-40) of the
+    RK4 trajectory of the reference RHS object, vs the oracle, fp64."""
+    n, dt, c = golden[f"ts_G{K}_{J}_meta"]
+    kw = dict(K=K, J=J, c=c, x0=golden[f"ts_G{K}_{J}_x0"], dt=dt, n_steps=int(n))
+    got = orc.forward(TwoScaleLorenz96Operator(**kw, arith="reference"), golden[f"ts_G{K}_{J}_u"])
+    assert np.array_equal(got, golden[f"ts_G{K}_{J}_G"])
+    fm = orc.forward(TwoScaleLorenz96Operator(**kw, arith="fma"), golden[f"ts_G{K}_{J}_u"])
+    np.testing.assert_allclose(fm, golden[f"ts_G{K}_{J}_G"], rtol=1e-9, atol=1e-10)
+
+
+def test_l96ts_moment_function_matches_reference(golden):
+    """The oracle's moment definition (reference mode: Ybar_k = Y_{k,0}, Q8) vs
+    moment_function itself on a random trajectory."""
+    Y, f = golden["ts_mom_y"], golden["ts_mom_f"]
+    K, J = 6, 4
+    X, Yb = Y[:K], Y[K::J][:K]
+    assert np.array_equal(np.concatenate([X, Yb, X * X, X * Yb, Yb * Yb]), f)
+
+
+def test_l96ts_chain_matches_reference_sampler(orc, golden):
+    K, J, n, dt, c, gamma, beta, seed, n_samples, burn_in, interval = golden["tsc_meta"]
+    op = TwoScaleLorenz96Operator(K=int(K), J=int(J), c=c, x0=golden["tsc_x0"], dt=dt, n_steps=int(n),
+                                  arith="reference")
+    samples, acc = _replay(orc, op, None, golden["tsc_y"], gamma, beta, int(seed), int(n_samples), int(burn_in),
+                           int(interval), 2, np.sqrt([10.0, 1.0, 10.0]))
+    assert np.array_equal(acc, golden["tsc_decisions"].sum(axis=1))
+    np.testing.assert_array_equal(samples, golden["tsc_samples"])
 
 
 # ---------------------------------------------------------------- Burgers
