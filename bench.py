@@ -16,7 +16,9 @@ algorithmic FLOP per launch / average kernel time from HIP events on the
 launch stream; algorithmic FLOP per pCN step per chain = 30·d·n = 2.4 MFLOP
 (SURVEY §8(d) counting rule).
 cpu_baseline: the C oracle (same arithmetic, bit-exact), a bounded sample of
-the same workload on this host's cores, rank 0 at N=1 only.
+the same workload on this host's cores, rank 0 at N=1 only; the reference
+itself, timed in the build container by tools/reference_cpu_baseline.py, is
+attached as cpu_baseline.reference_recorded.
 """
 import argparse
 import ctypes as C
@@ -169,7 +171,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=CHAINS_PER_GPU, help="chains per GPU")
+    ap.add_argument("--chains", type=int, default=CHAINS_PER_GPU, help="chains per GPU (weak) or in total (strong)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --chains per GPU (default); strong: --chains split over the GPUs")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -186,6 +190,10 @@ def main():
 
     log(f"rank {rank}/{world} on {dev}: building the problem")
     op, y = problem()
+    if args.scaling == "strong":
+        if args.chains % world:
+            raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
+        args.chains //= world  # chains per rank from here on
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     w = Workload(op, y, args.chains, rank * args.chains, tdt, dev, args.lanes)
     log(f"timing {args.steps} sweeps ({args.dtype}, {args.chains} chains/GPU, lanes={w.lanes})")
@@ -221,6 +229,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         log("CPU baseline (C oracle)")
         cpu = cpu_baseline(op, y, np.float64 if tdt == torch.float64 else np.float32)
+        ref_rec = os.path.join(REPO, "profiles", "r1", "reference_cpu_cfg3.json")
+        if os.path.exists(ref_rec):  # the reference itself, timed in the build container (tools/)
+            cpu["reference_recorded"] = json.load(open(ref_rec))
 
     if rank == 0:
         line = {
@@ -232,7 +243,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (forcing-field inverse problem, y = G(u_true) + N(0, 0.1^2), seed 3)",

@@ -173,6 +173,15 @@ int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t
 int ipmc_autocorr(const void* x, int32_t dtype, int64_t n_series, int64_t len, int64_t stride_series,
                   int64_t stride_t, int32_t max_lag, double* out, void* stream);
 
+/* Batched burn-in detection (len_burn_in, report/scripts/burgers/utilities.py:134-167):
+   chain c, variable v, sample t is x[c*stride_chain + v*stride_var + t*stride_t], t < len;
+   out[c] = the reference's burn-in index for that chain (window = avg_window = 50 and
+   threshold = accepted_change = 0.03 in the reference).  flags_scratch: uint32
+   [n_chains * ceil(len/32)] device scratch (overwritten).  Requires len >= window. */
+int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars, int64_t len, int64_t stride_chain,
+                 int64_t stride_var, int64_t stride_t, int32_t window, double threshold, uint32_t* flags_scratch,
+                 int64_t* out, void* stream);
+
 /* Layout the sweep kernel would use for this model/dtype when lanes_per_chain = chains_per_lane = 0:
    returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout. */
 int ipmc_auto_lanes(const ipmc_model* model, int32_t dtype, int64_t n_chains);

@@ -103,6 +103,11 @@ SIGNATURES = {
         C.c_int,
         [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p],
     ),
+    "ipmc_burn_in": (
+        C.c_int,
+        [C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32,
+         C.c_double, C.c_void_p, C.c_void_p, C.c_void_p],
+    ),
     "ipmc_auto_lanes": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_auto_layout": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_last_error": (C.c_char_p, []),

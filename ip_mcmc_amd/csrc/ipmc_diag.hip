@@ -64,9 +64,169 @@ __global__ __launch_bounds__(kAcBlock) void autocorr_kernel(const T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- burn-in
+// len_burn_in (burgers/utilities.py:134-167) for a batch of chains.  Per
+// chain c with n_vars series of len samples and window w:
+//   avg_v[j] = (cs[j+w-1] - cs[j-1]) / w   (cs = np.cumsum, cs[-1] := 0 term absent)
+//   changed[i] = any_v |(avg_v[i] - avg_v[i+1]) / mean_v| > thr,  i < L = len - w
+//   burn_in = largest i in [1, L-w-2] with changed[i..i+w] all set, else len-1.
+// Kernel 1: one thread per series (c, v) streams the series twice (the
+// leading and trailing cumulative sums are both sequential sums in np.cumsum's
+// order, so their difference is bit-identical to res[l:] - res[:-l]) and ORs
+// its flags into a per-chain bitmask.  Kernel 2: one thread per chain scans
+// the bitmask from the end.  All arithmetic is fp64.
+
+// numpy pairwise_sum (loops_utils.h.src) of a strided series, iteratively.
+template <typename T>
+__device__ double np_pairwise_strided(const T* a, int64_t n, int64_t s) {
+  int64_t off[48], len[48];
+  double left[48];
+  int stage[48];
+  int sp = 0;
+  off[0] = 0;
+  len[0] = n;
+  stage[0] = 0;
+  double ret = 0.0;
+  while (sp >= 0) {
+    const int64_t o = off[sp], m = len[sp];
+    if (m <= 128) {
+      const T* b = a + o * s;
+      if (m < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < m; ++i) r = r + (double)b[i * s];
+        ret = r;
+      } else {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = (double)b[j * s];
+        int64_t i;
+        for (i = 8; i < m - (m % 8); i += 8)
+          for (int j = 0; j < 8; ++j) r[j] = r[j] + (double)b[(i + j) * s];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < m; ++i) res = res + (double)b[i * s];
+        ret = res;
+      }
+      --sp;
+      continue;
+    }
+    int64_t n2 = m / 2;
+    n2 -= n2 % 8;
+    if (stage[sp] == 0) {
+      stage[sp] = 1;
+      ++sp;
+      off[sp] = o;
+      len[sp] = n2;
+      stage[sp] = 0;
+    } else if (stage[sp] == 1) {
+      left[sp] = ret;
+      stage[sp] = 2;
+      ++sp;
+      off[sp] = o + n2;
+      len[sp] = m - n2;
+      stage[sp] = 0;
+    } else {
+      ret = left[sp] + ret;
+      --sp;
+    }
+  }
+  return ret;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void burn_in_flags_kernel(const T* __restrict__ x, int64_t n_chains, int n_vars,
+                                                             int64_t len, int64_t s_chain, int64_t s_var,
+                                                             int64_t s_t, int w, double thr,
+                                                             unsigned* __restrict__ flags, int64_t words) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_chains * n_vars) return;
+  const int64_t c = g / n_vars;
+  const int v = (int)(g % n_vars);
+  const T* a = x + c * s_chain + v * s_var;
+  const double mean = np_pairwise_strided<T>(a, len, s_t) / (double)len;
+  const double dw = (double)w;
+  double lead = (double)a[0];
+  for (int64_t t = 1; t < w; ++t) lead = lead + (double)a[t * s_t];
+  double trail = 0.0;
+  double prev = lead / dw;
+  unsigned* fl = flags + c * words;
+  unsigned word = 0;
+  const int64_t L = len - w;
+  for (int64_t j = 1; j <= L; ++j) {
+    lead = lead + (double)a[(j + w - 1) * s_t];
+    trail = (j == 1) ? (double)a[0] : trail + (double)a[(j - 1) * s_t];
+    const double cur = (lead - trail) / dw;
+    const double ch = fabs((prev - cur) / mean);
+    const int64_t i = j - 1;
+    if (ch > thr) word |= 1u << (i & 31);
+    if ((i & 31) == 31 || j == L) {
+      if (word) atomicOr(fl + (i >> 5), word);
+      word = 0;
+    }
+    prev = cur;
+  }
+}
+
+__global__ void burn_in_search_kernel(int64_t n_chains, int64_t len, int w, const unsigned* __restrict__ flags,
+                                      int64_t words, int64_t* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_chains) return;
+  const unsigned* fl = flags + c * words;
+  const int64_t L = len - w;
+  const int64_t top = L - w - 2;
+  int64_t run = 0, res = len - 1;
+  for (int64_t j = L - 1; j >= 1; --j) {
+    run = ((fl[j >> 5] >> (j & 31)) & 1u) ? run + 1 : 0;
+    if (j <= top && run >= w + 1) {
+      res = j;
+      break;
+    }
+  }
+  out[c] = res;
+}
+
 }  // namespace ipmc
 
 using namespace ipmc;
+
+extern "C" int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars, int64_t len,
+                            int64_t stride_chain, int64_t stride_var, int64_t stride_t, int32_t window,
+                            double threshold, uint32_t* flags_scratch, int64_t* out, void* stream) {
+  if (n_chains < 0 || n_vars <= 0 || len < 0 || window <= 0) {
+    set_error("ipmc_burn_in: bad sizes (n_vars and window must be positive)");
+    return IPMC_ERR_INVALID;
+  }
+  if (n_chains == 0) return IPMC_OK;
+  if (len < window) {
+    set_error("ipmc_burn_in: series of %lld samples shorter than the window %d", (long long)len, window);
+    return IPMC_ERR_INVALID;
+  }
+  if (!x || !out || !flags_scratch) {
+    set_error("ipmc_burn_in: NULL pointer");
+    return IPMC_ERR_INVALID;
+  }
+  if (dtype != IPMC_F64 && dtype != IPMC_F32) {
+    set_error("ipmc_burn_in: bad dtype");
+    return IPMC_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t words = (len + 31) / 32;
+  if (hipMemsetAsync(flags_scratch, 0, (size_t)(n_chains * words) * sizeof(uint32_t), st) != hipSuccess) {
+    set_error("ipmc_burn_in: memset failed");
+    return IPMC_ERR_DEVICE;
+  }
+  const int64_t ns = n_chains * n_vars;
+  const unsigned nb = (unsigned)((ns + 255) / 256);
+  if (dtype == IPMC_F64)
+    hipLaunchKernelGGL(burn_in_flags_kernel<double>, dim3(nb), dim3(256), 0, st, (const double*)x, n_chains, n_vars,
+                       len, stride_chain, stride_var, stride_t, window, threshold, (unsigned*)flags_scratch, words);
+  else
+    hipLaunchKernelGGL(burn_in_flags_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, n_chains, n_vars,
+                       len, stride_chain, stride_var, stride_t, window, threshold, (unsigned*)flags_scratch, words);
+  int rc = check_launch("burn_in_flags_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(burn_in_search_kernel, dim3((unsigned)((n_chains + 255) / 256)), dim3(256), 0, st, n_chains, len,
+                     window, (const unsigned*)flags_scratch, words, out);
+  return check_launch("burn_in_search_kernel");
+}
 
 extern "C" int ipmc_autocorr(const void* x, int32_t dtype, int64_t n_series, int64_t len, int64_t stride_series,
                              int64_t stride_t, int32_t max_lag, double* out, void* stream) {

@@ -129,6 +129,63 @@ void orc_l96_rhs_f64(int32_t arith, int32_t d, const double* x, const double* F,
   l96_rhs_f64(arith == IPMC_ARITH_FMA, d, x, F, out);
 }
 
+/* numpy pairwise_sum (loops_utils.h.src) for any n, recursive as numpy's. */
+static double np_pairwise_any(const double* a, int64_t n) {
+  if (n <= 128) return np_pairwise_f64(a, (int)n);
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise_any(a, n2) + np_pairwise_any(a + n2, n - n2);
+}
+
+/* len_burn_in (report/scripts/burgers/utilities.py:134-167) for C chains of
+ * contiguous (n_vars, len) f64 blocks: moving_avg via np.cumsum
+ * (:139-142), means via np.mean (:155), changed flags (:156-159), search
+ * from the end (:162-165).  Returns 0, or -1 if len < window. */
+int orc_burn_in(const double* x, int64_t n_chains, int32_t n_vars, int64_t len, int32_t w, double thr,
+                int64_t* out) {
+  if (len < w || w <= 0) return -1;
+  const int64_t n_avgs = len - w + 1, L = n_avgs - 1;
+  double* cs = (double*)malloc(sizeof(double) * (size_t)len);
+  double* avgs = (double*)malloc(sizeof(double) * (size_t)(n_vars * n_avgs));
+  double* means = (double*)malloc(sizeof(double) * (size_t)n_vars);
+  unsigned char* ch = (unsigned char*)malloc((size_t)(L > 0 ? L : 1));
+  for (int64_t c = 0; c < n_chains; ++c) {
+    const double* xc = x + c * n_vars * len;
+    for (int v = 0; v < n_vars; ++v) {
+      const double* y = xc + v * len;
+      cs[0] = y[0];
+      for (int64_t t = 1; t < len; ++t) cs[t] = cs[t - 1] + y[t];
+      double* av = avgs + v * n_avgs;
+      av[0] = cs[w - 1] / (double)w;
+      for (int64_t j = 1; j < n_avgs; ++j) av[j] = (cs[j + w - 1] - cs[j - 1]) / (double)w;
+      means[v] = np_pairwise_any(y, len) / (double)len;
+    }
+    for (int64_t i = 0; i < L; ++i) {
+      int any = 0;
+      for (int v = 0; v < n_vars && !any; ++v) {
+        const double* av = avgs + v * n_avgs;
+        any = fabs((av[i] - av[i + 1]) / means[v]) > thr;
+      }
+      ch[i] = (unsigned char)any;
+    }
+    int64_t res = len - 1;
+    for (int64_t i = L - w - 2; i > 0; --i) {
+      int all = 1;
+      for (int64_t j = i; j < i + w + 1 && all; ++j) all = ch[j];
+      if (all) {
+        res = i;
+        break;
+      }
+    }
+    out[c] = res;
+  }
+  free(cs);
+  free(avgs);
+  free(means);
+  free(ch);
+  return 0;
+}
+
 /* Two-scale Lorenz-96 right-hand side (lorenz.py:44-101), fp64; p = (F, h, c, b). */
 void orc_l96ts_rhs_f64(int32_t arith, int32_t K, int32_t J, const double* x, const double* p, double* out) {
   const double hc = p[1] * p[2], hJ = p[1] / (double)J;

@@ -247,3 +247,17 @@ def rusanov_rate(w, dx, arith="reference"):
     r = np.zeros_like(w)
     lib().orc_rusanov_rate_f64(_abi.ARITH_FMA if arith == "fma" else _abi.ARITH_REFERENCE, w.size - 2, _p(w), dx, _p(r))
     return r
+
+
+def burn_in(x, window=50, threshold=0.03):
+    """len_burn_in for chains x of shape (C, n_vars, len) or (n_vars, len) (f64)."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    single = x.ndim == 2
+    if single:
+        x = x[None]
+    out = np.empty(x.shape[0], dtype=np.int64)
+    h = lib()
+    h.orc_burn_in.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_double, C.c_void_p]
+    rc = h.orc_burn_in(_p(x), x.shape[0], x.shape[1], x.shape[2], window, threshold, _p(out))
+    assert rc == 0, "series shorter than the window"
+    return int(out[0]) if single else out

@@ -440,6 +440,71 @@ def make_misc(out):
     out["ac_ref"] = np.stack([MCMCSampler.autocorr(x) for x in xs])
 
 
+def _reference_functions(path, names, namespace):
+    """Execute the named top-level function definitions of a reference script
+    (helpers.py / burgers/utilities.py import the absent POT package at module
+    level, so the module itself cannot be imported; the functions used here
+    need only numpy and MCMCSampler)."""
+    import ast
+
+    tree = ast.parse(open(path).read(), filename=path)
+    body = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in names]
+    assert sorted(n.name for n in body) == sorted(names)
+    exec(compile(ast.Module(body=body, type_ignores=[]), path, "exec"), namespace)
+    return namespace
+
+
+def _synthetic_chain(rng, n_vars, n):
+    """An MCMC-like trace: exponential relaxation from a far start onto a
+    stationary AR(1) around a mean (burn-in, then correlated noise)."""
+    mean = rng.uniform(0.2, 2, size=n_vars) * rng.choice([-1, 1], size=n_vars)
+    start = mean + rng.uniform(-3, 3, size=n_vars)
+    tau = rng.uniform(5, n / 3)
+    sig = 10 ** rng.uniform(-2.5, 0.3)
+    phi = rng.uniform(0.5, 0.995)
+    x = np.empty((n_vars, n))
+    e = np.zeros(n_vars)
+    for t in range(n):
+        e = phi * e + sig * rng.normal(size=n_vars)
+        x[:, t] = mean + (start - mean) * np.exp(-t / tau) + e
+    return x
+
+
+def make_burn_in(out):
+    """len_burn_in / uncorrelated_sample_spacing / clean_samples
+    (burgers/utilities.py:134-195) on synthetic traces."""
+    ns = {"np": np, "MCMCSampler": MCMCSampler}
+    _reference_functions(os.path.join(REF, "report", "scripts", "helpers.py"), ["autocorrelation"], ns)
+    _reference_functions(os.path.join(REF, "report", "scripts", "burgers", "utilities.py"),
+                         ["len_burn_in", "uncorrelated_sample_spacing", "clean_samples"], ns)
+    rng = np.random.default_rng(77)
+    sizes = [50, 51, 100, 153, 400, 1000, 1500, 3000]
+    i = 0
+    for n in sizes:
+        for n_vars in (1, 3):
+            x = np.ascontiguousarray(_synthetic_chain(rng, n_vars, n))
+            out[f"bi_x_{i}"] = x
+            out[f"bi_out_{i}"] = np.array(ns["len_burn_in"](x))
+            i += 1
+    # a chain whose moving average keeps changing (tiny mean) and a flat one
+    x = np.ascontiguousarray(np.stack([np.linspace(0, 1, 700), 1e-3 * rng.normal(size=700)]))
+    out[f"bi_x_{i}"], out[f"bi_out_{i}"] = x, np.array(ns["len_burn_in"](x))
+    i += 1
+    x = np.ones((2, 300))
+    out[f"bi_x_{i}"], out[f"bi_out_{i}"] = x, np.array(ns["len_burn_in"](x))
+    out["bi_count"] = np.array(i + 1)
+    # batch: 40 chains of 3 variables x 1200 samples
+    B = np.stack([_synthetic_chain(rng, 3, 1200) for _ in range(40)])
+    out["bi_batch_x"] = B
+    out["bi_batch_out"] = np.array([ns["len_burn_in"](np.ascontiguousarray(b)) for b in B])
+    # decorrelation spacing and the cleaned samples
+    for j, n in enumerate((400, 2000, 5000)):
+        x = np.ascontiguousarray(_synthetic_chain(rng, 3, n))
+        out[f"us_x_{j}"] = x
+        out[f"us_out_{j}"] = np.array(ns["uncorrelated_sample_spacing"](x))
+        out[f"cs_out_{j}"] = ns["clean_samples"](x)
+
+
 def main():
     out = {}
     make_l96(out)
@@ -449,6 +514,7 @@ def main():
     make_rw(out)
     make_burgers(out)
     make_misc(out)
+    make_burn_in(out)
     path = os.path.join(HERE, "reference_golden.npz")
     np.savez_compressed(path, **out)
     print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path)} bytes")

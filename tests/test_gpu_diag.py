@@ -44,3 +44,51 @@ def test_autocorrelation_windows_and_chain_layout():
     got = chain_autocorr(samples, 10)
     assert got.shape == (4, 5, 10)
     np.testing.assert_allclose(got[2, 3], MCMCSampler.autocorr(samples[2, :, 3])[:10], rtol=1e-10, atol=1e-12)
+
+
+# ------------------------------------------------------ burn-in (§8(f) #2)
+def test_burn_in_matches_reference_fixture(golden, orc):
+    """ipmc_burn_in vs the reference's len_burn_in (utilities.py:134-167): identical indices."""
+    from ip_mcmc_amd.diagnostics import burn_in_lengths, len_burn_in
+
+    for i in range(int(golden["bi_count"])):
+        assert len_burn_in(golden[f"bi_x_{i}"]) == int(golden[f"bi_out_{i}"]), i
+    B = golden["bi_batch_x"]
+    assert np.array_equal(burn_in_lengths(B), golden["bi_batch_out"])
+    # run()'s (C, n_samples, k) layout
+    assert np.array_equal(burn_in_lengths(np.ascontiguousarray(B.transpose(0, 2, 1)), layout="time_vars"),
+                          golden["bi_batch_out"])
+    # fp32 input: the oracle on the same fp32-rounded values
+    B32 = torch.as_tensor(B, dtype=torch.float32).cuda()
+    want = orc.burn_in(B32.double().cpu().numpy())
+    assert np.array_equal(burn_in_lengths(B32).cpu().numpy(), want)
+
+
+def test_burn_in_large_batch_vs_oracle(orc):
+    """65 536-chain-scale batch semantics on 2 048 chains x 4 vars x 3 000 samples."""
+    from ip_mcmc_amd.diagnostics import burn_in_lengths
+
+    rng = np.random.default_rng(5)
+    C, k, n = 2048, 4, 3000
+    t = np.arange(n)
+    drift = rng.uniform(1, 10, size=(C, k, 1)) * np.exp(-t / rng.uniform(30, 600, size=(C, 1, 1)))
+    x = 0.3 + drift + 0.05 * rng.normal(size=(C, k, n)).cumsum(axis=-1) / np.sqrt(t + 1)
+    got = burn_in_lengths(x)
+    assert np.array_equal(got, orc.burn_in(x))
+    assert len(set(got.tolist())) > 20
+
+
+def test_spacing_and_clean_samples_match_reference_fixture(golden):
+    from ip_mcmc_amd.diagnostics import clean_samples, uncorrelated_sample_spacing
+
+    for j in range(3):
+        x = golden[f"us_x_{j}"]
+        assert uncorrelated_sample_spacing(x) == int(golden[f"us_out_{j}"])
+        assert np.array_equal(clean_samples(x), golden[f"cs_out_{j}"])
+
+
+def test_burn_in_rejects_short_series():
+    from ip_mcmc_amd.diagnostics import burn_in_lengths
+
+    with pytest.raises(ValueError):
+        burn_in_lengths(np.zeros((2, 3, 49)))

@@ -254,3 +254,13 @@ def test_burgers_forward_reference_bit_exact(orc, golden, N):
     op_f = BurgersOperator(prior_mean=(0.0, 0.0, 0.0), N=N, T=1.0, dt_mode="cfl", arith="fma")
     np.testing.assert_allclose(orc.forward(op_f, golden[f"bur{N}_theta"]), golden[f"bur{N}_G"], rtol=1e-9,
                                atol=1e-12)
+
+
+# ------------------------------------------------------ burn-in (§8(f) #2)
+def test_burn_in_oracle_matches_reference(orc, golden):
+    """len_burn_in (burgers/utilities.py:134-167), run by make_golden.py on the
+    reference's own function, vs the C restatement: identical indices."""
+    for i in range(int(golden["bi_count"])):
+        assert orc.burn_in(golden[f"bi_x_{i}"]) == int(golden[f"bi_out_{i}"]), i
+    assert np.array_equal(orc.burn_in(golden["bi_batch_x"]), golden["bi_batch_out"])
+    assert len(set(golden["bi_batch_out"].tolist())) > 5, "fixture exercises too few outcomes"
