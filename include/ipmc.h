@@ -18,6 +18,13 @@
  *                                     stuart_examples.py:69-70,
  *                                     burgers/utilities.py:40-41
  *   GaussianDistribution.sample       distribution.py:114-118 ipmc_normal (counter-based N(0,I))
+ *   ConstStep/VarStepStandardRWProposer proposer.py:14-56     ipmc_sweep.proposal = IPMC_PROPOSAL_RW
+ *   StandardRWAccepter._I             accepter.py:104-106     ipmc_sweep.reg_scale, ipmc_init_phi
+ *   Lorenz96.__call__ (J > 0) + moment_function
+ *                                     lorenz.py:44-101,       IPMC_MODEL_LORENZ96_2S
+ *                                     lorenz_mcmc.py:17-40
+ *   MCMCSampler.autocorr              sampler.py:43-54        ipmc_autocorr
+ *   len_burn_in                       burgers/utilities.py:134-167  ipmc_burn_in
  *
  * The reference has no FFI of its own (it is duck-typed Python); these entry
  * points are what a ctypes binding of its plugin API binds.

@@ -1,9 +1,10 @@
 // Two-scale Lorenz-96 (lorenz.py:44-101 with J > 0) forward map, observed by
 // the time-averaged moment function of lorenz_mcmc.py:17-40, and its pCN sweep.
 //
-// Layout: one chain per group of GS lanes (GS = the power of two >= K, <= 64);
-// lane k < K owns the slow variable X_k and its fast block Y_{k,0..J-1} in
-// VGPRs (1+J values per RK4 array).  The fast blocks are cyclic inside the
+// Layout: one chain per group of K consecutive lanes, floor(64/K) chains per
+// wave (groups need not be power-of-two aligned: K=6 packs 10 chains = 60
+// live lanes per wave); lane k owns the slow variable X_k and its fast block
+// Y_{k,0..J-1} in VGPRs (1+J values per RK4 array).  The fast blocks are cyclic inside the
 // block (np.roll of Y_in[k, :]) so they never leave the lane; the slow
 // neighbours X_{k-2}, X_{k-1}, X_{k+1} (cyclic mod K) come by ds_bpermute.
 // theta = (F, h, b) = theta0 + u is the same on every lane of the group.
@@ -16,9 +17,28 @@ namespace ipmc {
 
 constexpr int kTsBlock = 256;
 
+// Occupancy target (waves per SIMD) for the sweep kernel: 4 RK4 arrays of
+// 1 + J values per lane plus the chain state.
+template <typename T, int J>
+constexpr int ts_waves() {
+  return sizeof(T) == 8 ? (J <= 4 ? 4 : (J <= 10 ? 3 : 2)) : (J <= 2 ? 5 : (J <= 10 ? 4 : 3));
+}
+
 struct TsCtx {
-  int K, GS, sub, base;  // base = first lane of the group
+  int K, sub, base;  // base = first lane of the group, sub = k
 };
+
+// lane -> (chain, k) for the packed layout; chain < 0 for the idle tail lanes.
+__device__ __forceinline__ int64_t ts_chain(int K, TsCtx& c) {
+  const int lane = threadIdx.x & 63;
+  const int cpw = 64 / K;
+  const int slot = lane / K;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  c.K = K;
+  c.sub = lane - slot * K;
+  c.base = slot * K;
+  return slot < cpw ? wave * cpw + slot : -1;
+}
 
 // numpy pairwise_sum order (n <= 128) of a compile-time-sized array.
 template <typename T, int J>
@@ -91,12 +111,14 @@ __device__ __forceinline__ void ts_rhs(const T (&s)[1 + J], T F, T hc, T hJ, T b
 }
 
 // Φ(theta0 + v) for the group; g_out (per chain, [5K]) receives G if set.
+// kq: k behind an opaque register copy made once per pCN step, so the
+// per-lane constants (x0 block, y, 1/gamma) are re-read each step instead of
+// being hoisted into VGPRs for the whole sweep.
 template <typename T, int J, bool FM>
-__device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, const T* __restrict__ y,
+__device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq, const T* __restrict__ y,
                     const T* __restrict__ ginv, T* g_out) {
   const int K = c.K;
-  const bool live = c.sub < K;
-  const int k = live ? c.sub : 0;
+  const int k = kq;
   const T* th0 = (const T*)m.theta0;
   const T F = th0[0] + v[0], h = th0[1] + v[1], bb = th0[2] + v[2];
   const T cc = (T)m.coupling_c;
@@ -148,7 +170,7 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, const 
 #pragma unroll
   for (int b = 0; b < 5; ++b) {
     const T g = ob[b] / nn;
-    if (g_out && live) g_out[b * K + k] = g;
+    if (g_out) g_out[b * K + k] = g;
     r[b] = y ? (y[b * K + k] - g) * ginv[b * K + k] : (T)0;
   }
   T s = (T)0;
@@ -165,12 +187,11 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, const 
 }
 
 template <typename T, int J, bool FM>
-__global__ __launch_bounds__(kTsBlock) void l96ts_sweep_kernel(const ipmc_model m, const ipmc_sweep s, int GS) {
+__global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
   const int lane = threadIdx.x & 63;
-  const int64_t tid = (int64_t)blockIdx.x * kTsBlock + threadIdx.x;
-  const int64_t chain = tid / GS;
-  const TsCtx c{m.dim, GS, (int)(tid % GS), lane & ~(GS - 1)};
-  if (chain >= s.n_chains) return;
+  TsCtx c;
+  const int64_t chain = ts_chain(m.dim, c);
+  if (chain < 0 || chain >= s.n_chains) return;
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
   T* u = (T*)s.u + chain * 3;
   T ur[3] = {u[0], u[1], u[2]};
@@ -184,6 +205,8 @@ __global__ __launch_bounds__(kTsBlock) void l96ts_sweep_kernel(const ipmc_model 
     const uint64_t step = s.step0 + (uint64_t)st;
     const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
     const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
+    int kq = c.sub;
+    asm volatile("" : "+v"(kq));
     T v[3];
     pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw);
     bool ok = true;
@@ -200,7 +223,7 @@ __global__ __launch_bounds__(kTsBlock) void l96ts_sweep_kernel(const ipmc_model 
     }
     if (ok) {
       ++ncalls;
-      T phv = ts_phi<T, J, FM>(m, v, c, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
+      T phv = ts_phi<T, J, FM>(m, v, c, kq, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
       if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
       if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
 #pragma unroll
@@ -235,33 +258,30 @@ __global__ __launch_bounds__(kTsBlock) void l96ts_sweep_kernel(const ipmc_model 
 template <typename T, int J, bool FM, bool PHI>
 __global__ __launch_bounds__(kTsBlock) void l96ts_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
                                                               const T* __restrict__ y, const T* __restrict__ ginv,
-                                                              T* __restrict__ out, int GS) {
-  const int lane = threadIdx.x & 63;
-  const int64_t tid = (int64_t)blockIdx.x * kTsBlock + threadIdx.x;
-  const int64_t chain = tid / GS;
-  const TsCtx c{m.dim, GS, (int)(tid % GS), lane & ~(GS - 1)};
-  if (chain >= n) return;
+                                                              T* __restrict__ out) {
+  TsCtx c;
+  const int64_t chain = ts_chain(m.dim, c);
+  if (chain < 0 || chain >= n) return;
   const T v[3] = {uin[chain * 3], uin[chain * 3 + 1], uin[chain * 3 + 2]};
-  const T ph = ts_phi<T, J, FM>(m, v, c, PHI ? y : nullptr, ginv, PHI ? nullptr : out + chain * m.q);
+  const T ph = ts_phi<T, J, FM>(m, v, c, c.sub, PHI ? y : nullptr, ginv, PHI ? nullptr : out + chain * m.q);
   if (PHI && c.sub == 0) out[chain] = ph;
 }
 
-static int group_size(int K) {
-  int g = 1;
-  while (g < K) g <<= 1;
-  return g;
+static int64_t ts_blocks(int K, int64_t n) {
+  const int64_t cpw = 64 / K;
+  const int64_t waves = (n + cpw - 1) / cpw;
+  return (waves * 64 + kTsBlock - 1) / kTsBlock;
 }
 
 #define IPMC_TS_J(X) X(1) X(2) X(4) X(8) X(10) X(16)
 
 template <typename T, bool FM>
 static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
-  const int GS = group_size(m.dim);
-  const int64_t blocks = (s.n_chains * GS + kTsBlock - 1) / kTsBlock;
+  const int64_t blocks = ts_blocks(m.dim, s.n_chains);
   switch (m.fast_per_slow) {
 #define IPMC_J(J)                                                                                             \
   case J:                                                                                                     \
-    hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, GS); \
+    hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s);     \
     return check_launch("l96ts_sweep_kernel");
     IPMC_TS_J(IPMC_J)
 #undef IPMC_J
@@ -273,17 +293,16 @@ static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) 
 template <typename T, bool FM>
 static int ts_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
                      bool phi, hipStream_t st) {
-  const int GS = group_size(m.dim);
-  const int64_t blocks = (n * GS + kTsBlock - 1) / kTsBlock;
+  const int64_t blocks = ts_blocks(m.dim, n);
   switch (m.fast_per_slow) {
 #define IPMC_J(J)                                                                                             \
   case J:                                                                                                     \
     if (phi)                                                                                                  \
       hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, true>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, \
-                         n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out, GS);                           \
+                         n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                               \
     else                                                                                                      \
       hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, false>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st,   \
-                         m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out, GS);                        \
+                         m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                            \
     return check_launch("l96ts_eval_kernel");
     IPMC_TS_J(IPMC_J)
 #undef IPMC_J

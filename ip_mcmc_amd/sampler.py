@@ -39,6 +39,17 @@ from .rng import PhiloxRNG, resolve_rng
 # pCN steps per chain in one kernel launch (launches are split at sample
 # boundaries; this bounds a single launch's run time for large ensembles).
 STEPS_PER_LAUNCH = 1024
+# ... and fewer for heavy ensembles: about LAUNCH_WORK state-component updates
+# per launch (~0.5 s on one MI355X; the headline sweep is 5.2e9 per step).
+LAUNCH_WORK = 8e11
+
+
+def _steps_per_launch(model, n_chains):
+    """pCN steps per launch so that one launch stays around half a second."""
+    rk = model.n_steps if model.n_steps > 0 else 1000
+    state = max(1, model.dim) * (1 + max(0, model.fast_per_slow))
+    per_step = float(n_chains) * rk * state
+    return int(max(1, min(STEPS_PER_LAUNCH, LAUNCH_WORK // max(per_step, 1.0))))
 
 
 class _Plan:
@@ -243,9 +254,10 @@ class MCMCSampler:
             prop_i += n
 
         t0 = time.perf_counter()
+        spl = _steps_per_launch(model, n_chains)
         n_burn = max(0, burn_in - sample_interval)  # sampler.py:18
-        for c0 in range(0, n_burn, STEPS_PER_LAUNCH):
-            launch(min(STEPS_PER_LAUNCH, n_burn - c0))
+        for c0 in range(0, n_burn, spl):
+            launch(min(spl, n_burn - c0))
 
         samples = None
         sums = None
@@ -269,7 +281,7 @@ class MCMCSampler:
             slot = i % buf_len
             done = 0
             while done < sample_interval:
-                n = min(STEPS_PER_LAUNCH, sample_interval - done)
+                n = min(spl, sample_interval - done)
                 last = done + n == sample_interval
                 view = samples[:, slot, :] if (samples is not None and last) else None
                 launch(n, view, sums)

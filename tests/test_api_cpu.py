@@ -157,3 +157,23 @@ def test_step_schedule_matches_reference(golden):
     """sampler.py:18-26 step count (fixture from the reference with MockProposer)."""
     for b, n, s, calls in golden["schedule"]:
         assert max(0, b - s) + n * s == calls
+
+
+def test_steps_per_launch_bounds_launch_work():
+    """Heavy ensembles are split into short launches; light ones use the cap."""
+    from ip_mcmc_amd import Lorenz96Operator, TwoScaleLorenz96Operator, _abi
+    from ip_mcmc_amd.sampler import STEPS_PER_LAUNCH, _steps_per_launch
+
+    def model(op):
+        m = _abi.IpmcModel()
+        for name, val in op._spec()[0].items():
+            setattr(m, name, val)
+        return m
+
+    head = Lorenz96Operator(40, 8.0, x0=np.full(40, 8.0), dt=0.005, n_steps=2000)
+    cfg5 = Lorenz96Operator(256, 8.0, x0=np.full(256, 8.0), dt=0.005, n_steps=10000)
+    assert _steps_per_launch(model(head), 65536) == 152  # 8e11 // 5.24e9
+    assert _steps_per_launch(model(cfg5), 131072) == 2
+    assert _steps_per_launch(model(head), 4) == STEPS_PER_LAUNCH
+    ts = TwoScaleLorenz96Operator(K=36, J=10, x0=np.zeros(396), n_steps=2000)
+    assert 1 <= _steps_per_launch(model(ts), 16384) < STEPS_PER_LAUNCH

@@ -562,3 +562,28 @@ def test_sampler_l96ts_chain_matches_reference_fixture(dev, golden):
     s = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(int(seed)))
     out = s.run(np.zeros((2, 3)), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
     assert np.array_equal(out, golden["tsc_samples"])
+
+
+def test_f32_and_f64_posterior_means_agree(dev):
+    """SURVEY §8(d) cfg 5 check on a mixing problem: the f32 and f64 kernels
+    give posterior means that agree within 4 standard errors (per-chain
+    agreement is impossible under chaos; the statistics must agree)."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, Lorenz96Operator,
+                             MCMCSampler, PhiloxRNG, pCNAccepter)
+
+    K = 8
+    op = Lorenz96Operator(K, 8.0, dt=0.01, n_steps=100)
+    ut = 0.5 * np.sin(2 * np.pi * np.arange(K) / K)
+    y = op(ut) + 0.1 * np.random.default_rng(0).normal(size=K)
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(K), 0.01 * np.eye(K)))
+    prior = GaussianDistribution(np.zeros(K), np.eye(K))
+    C = 16384
+    means, ses = [], []
+    for dtype in (np.float32, np.float64):
+        s = MCMCSampler(ConstSteppCNProposer(0.2, prior), pCNAccepter(pot), PhiloxRNG(11), dtype=dtype)
+        last = s.run(np.zeros((C, K)), n_samples=1, burn_in=600, sample_interval=1, keep="last")
+        last = np.asarray(last, dtype=np.float64).reshape(C, K)
+        means.append(last.mean(axis=0))
+        ses.append(last.std(axis=0) / np.sqrt(C))
+    z = np.abs(means[0] - means[1]) / np.sqrt(ses[0] ** 2 + ses[1] ** 2)
+    assert np.all(z < 4), z

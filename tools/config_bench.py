@@ -7,6 +7,8 @@ cfg4     Burgers N=256, fixed dt 1e-3 x 1000, 2 048 chains (= 16 384 / 8 GPUs)
 cfg4full Burgers as cfg4 with all 16 384 chains on one GPU
 cfg4cfl  Burgers N=256, reference CFL time stepping, 2 048 chains
 cfg5     Lorenz-96 d=256, 10 000 RK4 steps, 131 072 chains (= 2^20 / 8 GPUs)
+ts6      two-scale Lorenz-96 K=6 J=4 (the thesis problem, lorenz_mcmc.py:87-88), T=20 (4 000 RK4 steps), 65 536 chains
+ts36     two-scale Lorenz-96 K=36 J=10, 2 000 RK4 steps of 0.002, 16 384 chains
 """
 import ctypes as C
 import json
@@ -18,7 +20,8 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from ip_mcmc_amd import BurgersOperator, Lorenz63Operator, Lorenz96Operator, _abi  # noqa: E402
+from ip_mcmc_amd import (BurgersOperator, Lorenz63Operator, Lorenz96Operator, TwoScaleLorenz96Operator,  # noqa: E402
+                         _abi)
 from ip_mcmc_amd._lib import call, lib  # noqa: E402
 
 
@@ -37,6 +40,12 @@ def make(cfg):
     if cfg == "cfg5":
         op = Lorenz96Operator(256, 8.0, dt=0.005, n_steps=10000)
         return op, 131072, 0.2, np.ones(256), 30 * 256 * 10000, 0.1
+    if cfg == "ts6":
+        op = TwoScaleLorenz96Operator(K=6, J=4, dt=0.005, n_steps=4000)
+        return op, 65536, 0.5, np.sqrt([10.0, 1.0, 10.0]), 45 * 30 * 4000, 0.5
+    if cfg == "ts36":
+        op = TwoScaleLorenz96Operator(K=36, J=10, dt=0.002, n_steps=2000, moments="mean")
+        return op, 16384, 0.5, np.sqrt([10.0, 1.0, 10.0]), 45 * 396 * 2000, 0.5
     raise SystemExit(f"unknown config {cfg}")
 
 
