@@ -20,20 +20,27 @@ namespace ipmc {
 
 constexpr int kBurBlock = 256;
 
-template <typename T, bool FM>
-__device__ __forceinline__ T rus_flux(T a, T b) {
+// Rusanov flux F = ½(f(a)+f(b)) − ½·max(|a|,|b|)·(b−a), f(w) = w²/2
+// (rusanov.py:92-96), REFERENCE arith: the reference's operation order.
+template <typename T>
+__device__ __forceinline__ T rus_flux_ref(T a, T b) {
   const T half = (T)0.5;
   const T aa = a < (T)0 ? -a : a, ab = b < (T)0 ? -b : b;
   const T sp = ab > aa ? ab : aa;
-  if constexpr (FM) {
-    const T fb = (half * b) * b;
-    const T favg = half * madd<true>(half * a, a, fb);
-    return madd<true>(-(half * sp), b - a, favg);
-  } else {
-    const T fa = (half * a) * a, fb = (half * b) * b;
-    const T favg = half * (fa + fb);
-    return favg - (half * sp) * (b - a);
-  }
+  const T fa = (half * a) * a, fb = (half * b) * b;
+  const T favg = half * (fa + fb);
+  return favg - (half * sp) * (b - a);
+}
+
+// FMA arith: the flux pre-scaled by 1/(−dx), F̃ = fma(c2·s, b−a, c1·(a²+b²))
+// with c1 = ¼/(−dx), c2 = −½/(−dx), so dudt = F̃_{i+½} − F̃_{i−½} needs no
+// division (7 VALU ops per interface).  max is fmax: equal to the reference's
+// max for every non-NaN pair.
+template <typename T>
+__device__ __forceinline__ T rus_flux_fm(T a, T b, T c1, T c2) {
+  const T sp = __builtin_fmax(__builtin_fabs(a), __builtin_fabs(b));
+  const T sq = madd<true>(b, b, a * a);
+  return madd<true>(c2 * sp, b - a, c1 * sq);
 }
 
 template <int GS, typename T>
@@ -41,37 +48,43 @@ __device__ __forceinline__ T group_max_abs(T m) {
 #pragma unroll
   for (int off = GS / 2; off >= 1; off >>= 1) {
     const T o = __shfl_xor(m, off, 64);
-    m = (o > m) ? o : m;
+    m = __builtin_fmax(o, m);
   }
   return m;
 }
 
+// max |w| over the lane's cells (NaN ignored, as the reference's np.max of a
+// finite state never sees one before the CFL guard trips)
 template <int CPL, typename T>
 __device__ __forceinline__ T lane_max_abs(const T (&w)[CPL], bool live) {
   T m = (T)0;
   if (live) {
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const T a = w[j] < (T)0 ? -w[j] : w[j];
-      if (a > m) m = a;
-    }
+    for (int j = 0; j < CPL; ++j) m = __builtin_fmax(m, __builtin_fabs(w[j]));
   }
   return m;
 }
 
 // dudt for the lane's cells from state s (+ halos hl / hr).
+// k.mdx = −dx (REFERENCE divides by it); k.c1, k.c2: the FMA flux scales.
+template <typename T>
+struct RusConst {
+  T mdx, c1, c2, nudx2;
+};
+
 template <typename T, int CPL, bool FM>
-__device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, T mdx, T nudx2, bool visc, T (&r)[CPL]) {
-  T fl = rus_flux<T, FM>(hl, s[0]);
+__device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const RusConst<T>& k, bool visc,
+                                         T (&r)[CPL]) {
+  T fl = FM ? rus_flux_fm<T>(hl, s[0], k.c1, k.c2) : rus_flux_ref<T>(hl, s[0]);
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const T right = (j + 1 < CPL) ? s[j + 1] : hr;
     const T left = (j > 0) ? s[j - 1] : hl;
-    const T fr = rus_flux<T, FM>(s[j], right);
-    T v = (fr - fl) / mdx;
+    const T fr = FM ? rus_flux_fm<T>(s[j], right, k.c1, k.c2) : rus_flux_ref<T>(s[j], right);
+    T v = FM ? fr - fl : (fr - fl) / k.mdx;
     if (visc) {
       const T lap = (right - (s[j] + s[j])) + left;
-      v = madd<FM>(nudx2, lap, v);
+      v = madd<FM>(k.nudx2, lap, v);
     }
     r[j] = v;
     fl = fr;
@@ -84,10 +97,15 @@ struct BurCtx {
 
 // Halo exchange inside the group: value of the previous lane's last cell and
 // the next lane's first cell (or the ghosts at the ends).
+// DPP wave_shr:1 / wave_shl:1 (GFX9 whole-wave shifts; no LDS round trip):
+// the lanes they leave without a source are group ends, which take ghosts.
+constexpr int kDppWaveShl1 = 0x130;
+constexpr int kDppWaveShr1 = 0x138;
+
 template <typename T, int CPL>
 __device__ __forceinline__ void halos(const T (&s)[CPL], T gl, T gr, const BurCtx& c, T& hl, T& hr) {
-  hl = __shfl(s[CPL - 1], c.lane - 1, 64);
-  hr = __shfl(s[0], c.lane + 1, 64);
+  hl = dpp<kDppWaveShr1>(s[CPL - 1]);
+  hr = dpp<kDppWaveShl1>(s[0]);
   if (c.sub == 0) hl = gl;
   if (c.sub == c.nlive - 1) hr = gr;
 }
@@ -110,7 +128,8 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   const T dx = (T)m.dx, mdx = -dx;
   const T cfl_dx = (T)m.cfl * dx;
   const bool visc = (m.nu != 0.0);
-  const T nudx2 = (T)m.nu / (dx * dx);
+  const T rdx = (T)1 / mdx;
+  const RusConst<T> kc{mdx, (T)0.25 * rdx, (T)-0.5 * rdx, (T)m.nu / (dx * dx)};
   const T tend = (T)m.t_end;
   const T dtf = (T)m.dt;
   const bool cflmode = (m.dt_mode == IPMC_DT_CFL);
@@ -139,12 +158,12 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
     // SSPRK2, rusanov.py:62-74
     T hl, hr, r[CPL], ws[CPL];
     halos<T, CPL>(w, gl, gr, c, hl, hr);
-    rus_rate<T, CPL, FM>(w, hl, hr, mdx, nudx2, visc, r);
+    rus_rate<T, CPL, FM>(w, hl, hr, kc, visc, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) ws[j] = madd<FM>(dt, r[j], w[j]);
     const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
     halos<T, CPL>(ws, gls, grs, c, hl, hr);
-    rus_rate<T, CPL, FM>(ws, hl, hr, mdx, nudx2, visc, r);
+    rus_rate<T, CPL, FM>(ws, hl, hr, kc, visc, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       ws[j] = madd<FM>(dt, r[j], ws[j]);
@@ -323,23 +342,29 @@ __global__ __launch_bounds__(kBurBlock) void burgers_eval_kernel(const ipmc_mode
 
 // ------------------------------------------------------------------ host
 // Supported layouts: CPL cells per lane, GS lanes per chain.
-static bool pick(int N, int64_t n_chains, int& cpl, int& gs) {
-  // Prefer 8 cells per lane; fall back to 4 when a chain does not fill 8-cell lanes.
-  const int cands[2] = {8, 4};
-  for (int c : cands) {
-    if (N % c) continue;
-    const int need = N / c;
-    const int groups[3] = {16, 32, 64};
-    for (int g : groups) {
-      if (need <= g) {
-        cpl = c;
-        gs = g;
-        return true;
-      }
+static bool fit(int N, int c, int& cpl, int& gs) {
+  if (N % c) return false;
+  const int need = N / c;
+  const int groups[3] = {16, 32, 64};
+  for (int g : groups) {
+    if (need <= g) {
+      cpl = c;
+      gs = g;
+      return true;
     }
   }
-  (void)n_chains;
   return false;
+}
+
+// Prefer 8 cells per lane (more independent work per lane between halo
+// exchanges); 4 when a chain does not fit 8-cell lanes.  Measured on cfg 4
+// (N=256): 8 cells beat 4 even for 2 048 chains, where 4 would double the
+// waves per SIMD (profiles/r1/configs.jsonl).  lanes_per_chain > 0
+// (ipmc_sweep) forces CPL = N / lanes_per_chain.
+static bool pick(int N, int64_t n_chains, int lanes, int& cpl, int& gs) {
+  (void)n_chains;
+  if (lanes > 0) return (N % lanes == 0) && fit(N, N / lanes, cpl, gs);
+  return fit(N, 8, cpl, gs) || fit(N, 4, cpl, gs);
 }
 
 template <typename T, int CPL, int GS, bool FM>
@@ -371,13 +396,14 @@ static int dispatch(int cpl, int gs, F&& f) {
   return IPMC_ERR_UNSUPPORTED;
 }
 
-static int validate(const ipmc_model& m, int64_t n_chains, int& cpl, int& gs) {
+static int validate(const ipmc_model& m, int64_t n_chains, int lanes, int& cpl, int& gs) {
   if (m.q > kBurQMax) {
     set_error("Burgers: at most %d observation windows", kBurQMax);
     return IPMC_ERR_UNSUPPORTED;
   }
-  if (!pick(m.dim, n_chains, cpl, gs)) {
-    set_error("Burgers: N=%d must be a multiple of 4 and at most 512", m.dim);
+  if (!pick(m.dim, n_chains, lanes, cpl, gs) || (cpl != 4 && cpl != 8)) {
+    set_error("Burgers: N=%d must be a multiple of 4 and at most 512 (lanes_per_chain=%d: N/lanes must be 4 or 8)",
+              m.dim, lanes);
     return IPMC_ERR_UNSUPPORTED;
   }
   return IPMC_OK;
@@ -408,7 +434,7 @@ struct EvalLauncher {
 
 int burgers_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
   int cpl, gs;
-  int rc = validate(m, s.n_chains, cpl, gs);
+  int rc = validate(m, s.n_chains, s.lanes_per_chain, cpl, gs);
   if (rc) return rc;
   SweepLauncher l{m, s, st};
   const bool fm = m.arith == IPMC_ARITH_FMA;
@@ -419,7 +445,7 @@ int burgers_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
 int burgers_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
                  void* out, bool phi, hipStream_t st) {
   int cpl, gs;
-  int rc = validate(m, n, cpl, gs);
+  int rc = validate(m, n, 0, cpl, gs);
   if (rc) return rc;
   EvalLauncher l{m, n, u, y, ginv, out, phi, st};
   const bool fm = m.arith == IPMC_ARITH_FMA;

@@ -26,18 +26,22 @@
 #define REAL double
 #define SFX(n) n##_f64
 #define FMA(a, b, c) fma((a), (b), (c))
+#define FMAX(a, b) fmax((a), (b))
 #include "orc_models.inc"
 #undef REAL
 #undef SFX
 #undef FMA
+#undef FMAX
 
 #define REAL float
 #define SFX(n) n##_f32
 #define FMA(a, b, c) fmaf((a), (b), (c))
+#define FMAX(a, b) fmaxf((a), (b))
 #include "orc_models.inc"
 #undef REAL
 #undef SFX
 #undef FMA
+#undef FMAX
 
 static int check_model(const ipmc_model* m) {
   if (!m || m->k <= 0 || m->q <= 0) return IPMC_ERR_INVALID;
@@ -194,7 +198,7 @@ void orc_l96ts_rhs_f64(int32_t arith, int32_t K, int32_t J, const double* x, con
 
 /* Rusanov pieces for the rusanov.py:112-170 known-answer tests. */
 double orc_rusanov_flux_f64(int32_t arith, double a, double b) {
-  return rus_flux_f64(arith == IPMC_ARITH_FMA, a, b);
+  return arith == IPMC_ARITH_FMA ? rus_flux_fm_f64(a, b, 0.25, -0.5) : rus_flux_f64(a, b);
 }
 void orc_rusanov_rate_f64(int32_t arith, int32_t N, const double* w, double dx, double* r) {
   rus_rate_f64(arith == IPMC_ARITH_FMA, N, w, -dx, 0.0, 0, r);

@@ -587,3 +587,17 @@ def test_f32_and_f64_posterior_means_agree(dev):
         ses.append(last.std(axis=0) / np.sqrt(C))
     z = np.abs(means[0] - means[1]) / np.sqrt(ses[0] ** 2 + ses[1] ** 2)
     assert np.all(z < 4), z
+
+
+def test_burgers_every_layout_bit_exact(dev, orc):
+    """Both cells-per-lane layouts (8 and 4) of the Burgers kernel give the oracle's bits."""
+    from ip_mcmc_amd import BurgersOperator
+
+    for N, lanes_list in ((128, (16, 32)), (256, (32, 64))):
+        for arith in ("fma", "reference"):
+            op = BurgersOperator(N=N, dt_mode="cfl", arith=arith)
+            U0, phi0, y, ginv, sq = _problem(op, 40, torch.float64, orc, seed=N)
+            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, torch.float64)
+            for lanes in lanes_list:
+                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, torch.float64, dev, lanes=lanes)
+                _assert_same(d, o, (N, arith, lanes))

@@ -49,7 +49,7 @@ def make(cfg):
     raise SystemExit(f"unknown config {cfg}")
 
 
-def run(cfg, dtype, steps=3):
+def run(cfg, dtype, steps=3, lanes=0):
     dev = torch.device("cuda", 0)
     op, n, beta, sq, flop, gamma = make(cfg)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
@@ -64,7 +64,7 @@ def run(cfg, dtype, steps=3):
     call("ipmc_potential", C.byref(m), adt, n, u.data_ptr(), y.data_ptr(), gi.data_ptr(), phi.data_ptr(), st)
     acc = torch.zeros(n, dtype=torch.int64, device=dev)
     s = _abi.IpmcSweep()
-    s.dtype, s.n_chains = adt, n
+    s.dtype, s.n_chains, s.lanes_per_chain = adt, n, lanes
     s.u, s.phi, s.accepts = u.data_ptr(), phi.data_ptr(), acc.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = y.data_ptr(), gi.data_ptr(), sqt.data_ptr()
     s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
@@ -89,6 +89,8 @@ def run(cfg, dtype, steps=3):
         "tflops_algorithmic": n * flop / (ms * 1e-3) / 1e12,
         "accept_rate": float(acc.sum().item()) / (n * (steps + 1)),
     }
+    if lanes:
+        res["lanes_forced"] = lanes
     if isinstance(op, Lorenz96Operator):
         res["lanes_per_chain"] = lib().ipmc_auto_lanes(C.byref(m), adt, n)
     print(json.dumps(res), flush=True)
@@ -96,6 +98,7 @@ def run(cfg, dtype, steps=3):
 
 if __name__ == "__main__":
     cfgs = sys.argv[1:] or ["cfg2", "cfg4", "cfg4full", "cfg4cfl", "cfg5"]
-    for c in cfgs:
+    for c in cfgs:  # "cfg4:64" forces 64 lanes per chain
+        name, _, lanes = c.partition(":")
         for dt in (torch.float64, torch.float32):
-            run(c, dt)
+            run(name, dt, lanes=int(lanes or 0))
