@@ -204,11 +204,6 @@ __device__ T trapz_pairwise(const T* v, int n, T mdx) {
   return res;
 }
 
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // G(theta) for the chain, state staged through `row` (this chain's N
 // interior cells in LDS).  Lane 0 of the group evaluates the windows and,

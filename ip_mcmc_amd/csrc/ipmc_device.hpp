@@ -244,6 +244,13 @@ __device__ __forceinline__ T group_bcast(T v, int lane) {
   }
 }
 
+// LDS written by lanes of this wavefront is visible to the whole wavefront.
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // All lanes of the group hold `ok`: true iff every lane's ok is true.
 template <int LPC>
 __device__ __forceinline__ bool group_all(bool ok, int lane) {

@@ -87,10 +87,19 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
   for (int j = 0; j < M; ++j) g[j] = ob[j] / nn;
 }
 
+constexpr int kL96Block = 256;
+
+// LDS staging for the in-order misfit / regularizer sums of wide groups
+// (LPC >= 8, group_sumsq); one element otherwise.
+template <int M, int LPC>
+constexpr int l96_stage_len() {
+  return LPC >= 8 ? M * kL96Block : 1;
+}
+
 template <typename V, int M, int LPC, bool FM, typename S>
 __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict__ th0, const S* __restrict__ x0,
                                            const S* __restrict__ y, const S* __restrict__ ginv, V h, int nsteps,
-                                           int lane) {
+                                           int lane, V* stage) {
   using P = Splat<V>;
   V F[M], g[M];
 #pragma unroll
@@ -99,18 +108,29 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
   V r[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) r[j] = (P::of(y[j]) - g[j]) * P::of(ginv[j]);
-  return P::of((S)0.5) * ordered_sumsq<V, M, LPC, FM>(r, lane, P::of((S)0));
+  return P::of((S)0.5) * group_sumsq<V, M, LPC, FM, kL96Block>(r, lane, stage, P::of((S)0));
 }
-
-constexpr int kL96Block = 256;
 
 // Occupancy target (waves per SIMD) the register allocator is held to: the
 // state needs ~6 arrays of M values live in the RK loop (x, F, time-average,
 // k-sum, stage, rhs), plus ~40 registers of addressing / RNG / loop state.
+// (fp32 one chain per lane group: the compiler's SLP packing needs ~96; every
+// variant gets at least 96 registers, i.e. at most 5 waves, since the
+// proposal / accept stage spills below that.)
 template <typename T, int M>
 constexpr int l96_waves_per_simd() {
-  constexpr int regs = 6 * M * (int)(sizeof(T) / 4) + 40;
+  constexpr int want = 6 * M * (int)(sizeof(T) / 4) + (sizeof(T) == 8 ? 40 : 96);
+  constexpr int regs = want < 96 ? 96 : want;
   constexpr int w = 512 / regs;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+// The packed fp32 kernel carries two chains' proposal/accept state (~76
+// registers, measured: <40,4> needs 196 VGPRs); holding it to fewer spills
+// to scratch, so its target is set from 12·M + 76.
+template <int M>
+constexpr int l96_pk_waves_per_simd() {
+  constexpr int w = 512 / (12 * M + 76);
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
@@ -119,6 +139,7 @@ template <typename T, int D, int LPC, bool FM>
 __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void l96_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
   constexpr int M = D / LPC;
   __shared__ T vpark[M][kL96Block];  // proposal parked in LDS while G runs
+  __shared__ T stage[l96_stage_len<M, LPC>()];
   const int lane = threadIdx.x & 63;
   const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
   const int64_t chain = tid / LPC;
@@ -145,11 +166,13 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
     pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw);
     if (box_valid<T, M, LPC>(s, c0, v, lane)) {
       ++ncalls;
-      const T reg = s.reg_scale ? regularizer<T, M, LPC, FM>((const T*)s.reg_scale + cl, v, lane) : (T)0;
+      const T reg = s.reg_scale
+                        ? regularizer<T, M, LPC, FM, T, kL96Block>((const T*)s.reg_scale + cl, v, lane, stage)
+                        : (T)0;
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x] = v[j];
       T phv = l96_potential<T, M, LPC, FM>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
-                                           (const T*)s.gamma_inv + cl, h, m.n_steps, lane);
+                                           (const T*)s.gamma_inv + cl, h, m.n_steps, lane, stage);
       if (s.reg_scale) phv = phv + reg;  // I(v) = Φ(v) + regularizer (accepter.py:106)
       // memory clobber: re-read v from LDS instead of keeping it live in VGPRs across G
       asm volatile("" ::: "memory");
@@ -187,11 +210,12 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
 // runs on f32x2 so every FLOP is a v_pk_*_f32; proposal and accept stay per
 // chain (scalar), so the bits equal the one-chain kernel's.
 template <int D, int LPC, bool FM>
-__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<double, D / LPC>())) void l96_sweep_pk_kernel(
+__global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void l96_sweep_pk_kernel(
     const ipmc_model m, const ipmc_sweep s) {
   constexpr int M = D / LPC;
   using V = f32x2;
   __shared__ V vpark[M][kL96Block];
+  __shared__ V stage[l96_stage_len<M, LPC>()];
   const int lane = threadIdx.x & 63;
   const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
   const int64_t pair = tid / LPC;
@@ -216,24 +240,38 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<double, D / LPC>()))
     const float bs = s.beta_schedule ? (float)s.beta_schedule[2 * st] : beta;
     const float cs = s.beta_schedule ? (float)s.beta_schedule[2 * st + 1] : contr;
     const float* sq = (const float*)s.prior_sqrt + cl;
-    float va[M], vb[M];
     const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
-    pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va, rw);
-    pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb, rw);
-    const bool oka = box_valid<float, M, LPC>(s, c0, va, lane);
-    const bool okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
+    // propose A, park it, then B: one chain's proposal live at a time (the
+    // two-chain proposal stage otherwise spills past the occupancy target)
+    bool oka, okb;
+    {
+      float va[M];
+      pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va, rw);
+      oka = box_valid<float, M, LPC>(s, c0, va, lane);
+#pragma unroll
+      for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].x = va[j];
+    }
+    asm volatile("" ::: "memory");
+    {
+      float vb[M];
+      pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb, rw);
+      okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
+#pragma unroll
+      for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].y = vb[j];
+    }
+    asm volatile("" ::: "memory");
     if (oka || okb) {
       ka += oka;
       kb += okb;
       V v[M];
 #pragma unroll
-      for (int j = 0; j < M; ++j) v[j] = V{va[j], vb[j]};
-      const V reg = s.reg_scale ? regularizer<V, M, LPC, FM>((const float*)s.reg_scale + cl, v, lane) : V{0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < M; ++j) vpark[j][threadIdx.x] = v[j];
+      for (int j = 0; j < M; ++j) v[j] = vpark[j][threadIdx.x];
+      const V reg = s.reg_scale
+                        ? regularizer<V, M, LPC, FM, float, kL96Block>((const float*)s.reg_scale + cl, v, lane, stage)
+                        : V{0.f, 0.f};
       V ph = l96_potential<V, M, LPC, FM>(v, (const float*)m.theta0 + cl, (const float*)m.x0 + cl,
                                           (const float*)s.y + cl, (const float*)s.gamma_inv + cl, h, m.n_steps,
-                                          lane);
+                                          lane, stage);
       if (s.reg_scale) ph = ph + reg;
       asm volatile("" ::: "memory");
       if (oka && pcn_accept<float>(pa, ph.x, s.seed, ga, step)) {
@@ -291,6 +329,7 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
                                                               const T* __restrict__ yin,
                                                               const T* __restrict__ ginvin, T* __restrict__ out) {
   constexpr int M = D / LPC;
+  __shared__ T stage[PHI ? l96_stage_len<M, LPC>() : 1];
   const int lane = threadIdx.x & 63;
   const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
   const int64_t chain = tid / LPC;
@@ -305,7 +344,7 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
 #pragma unroll
   for (int j = 0; j < M; ++j) v[j] = u[j];
   if constexpr (PHI) {
-    const T ph = l96_potential<T, M, LPC, FM>(v, th0, x0, yin + c0, ginvin + c0, h, m.n_steps, lane);
+    const T ph = l96_potential<T, M, LPC, FM>(v, th0, x0, yin + c0, ginvin + c0, h, m.n_steps, lane, stage);
     if (sub == 0) out[chain] = ph;
   } else {
     T F[M], g[M];

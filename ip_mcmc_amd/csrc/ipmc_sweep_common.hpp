@@ -62,16 +62,46 @@ __device__ __forceinline__ T ordered_sumsq(const T (&r)[M], int lane, T s) {
   }
 }
 
+// The same in-order sum through LDS for wide groups (LPC >= 8): each lane
+// parks its M values in `stage` (M rows of BLK, this thread's column) and every
+// lane of the group reads the chain's LPC*M values back in order -- broadcast
+// LDS reads instead of LPC*M cross-lane moves, which the compiler would issue
+// all at once and spill (d = 256: 345 VGPRs of spill without this).
+template <typename V, int M, int LPC, bool FM, int BLK>
+__device__ __forceinline__ V ordered_sumsq_lds(const V (&r)[M], V* stage, V s) {
+  const int t = threadIdx.x;
+  const int base = t & ~(LPC - 1);
+#pragma unroll
+  for (int j = 0; j < M; ++j) stage[j * BLK + t] = r[j];
+  wave_sync_lds();
+#pragma unroll 1
+  for (int sub = 0; sub < LPC; ++sub) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const V x = stage[j * BLK + base + sub];
+      s = madd<FM>(x, x, s);
+    }
+  }
+  wave_sync_lds();  // the stage is reused by the next sum
+  return s;
+}
+
+template <typename V, int M, int LPC, bool FM, int BLK>
+__device__ __forceinline__ V group_sumsq(const V (&r)[M], int lane, V* stage, V s) {
+  if constexpr (LPC >= 8 && BLK > 0) return ordered_sumsq_lds<V, M, LPC, FM, BLK>(r, stage, s);
+  else return ordered_sumsq<V, M, LPC, FM>(r, lane, s);
+}
+
 // StandardRWAccepter regularizer ½ Σ_i (c_i v_i)² over the chain's components
 // in component order (accepter.py:104-106 with the reference's sqrt-covariance
 // factor); c = reg_scale + this lane's offset.
-template <typename V, int M, int LPC, bool FM, typename S>
-__device__ __forceinline__ V regularizer(const S* __restrict__ c, const V (&v)[M], int lane) {
+template <typename V, int M, int LPC, bool FM, typename S, int BLK = 0>
+__device__ __forceinline__ V regularizer(const S* __restrict__ c, const V (&v)[M], int lane, V* stage = nullptr) {
   using P = Splat<V>;
   V t[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) t[j] = P::of(c[j]) * v[j];
-  return P::of((S)0.5) * ordered_sumsq<V, M, LPC, FM>(t, lane, P::of((S)0));
+  return P::of((S)0.5) * group_sumsq<V, M, LPC, FM, BLK>(t, lane, stage, P::of((S)0));
 }
 
 // ConstrainAccepter box: lo < v + off < hi for every component of the chain.
