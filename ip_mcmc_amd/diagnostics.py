@@ -105,7 +105,7 @@ def len_burn_in(x, device=None):
 
 
 def uncorrelated_sample_spacing(x, device=None):
-    """utilities.py:170-187: grow tau by 1.5x from 10 until the variable-averaged
+    """utilities.py:169-186: grow tau by 1.5x from 10 until the variable-averaged
     windowed autocorrelation first drops to <= 0.001; returns that lag.  Keeps
     the reference's early exit value len(x) (the number of variables)
     when the series is too short to decorrelate."""
@@ -123,7 +123,7 @@ def uncorrelated_sample_spacing(x, device=None):
 
 
 def clean_samples(x, device=None):
-    """utilities.py:190-195: drop the burn-in, then keep every spacing-th sample."""
+    """utilities.py:189-195: drop the burn-in, then keep every spacing-th sample."""
     x_ = np.copy(np.asarray(x, dtype=np.float64))
     x_ = x_[:, len_burn_in(x_, device):]
     return x_[:, :: uncorrelated_sample_spacing(x_, device)]
