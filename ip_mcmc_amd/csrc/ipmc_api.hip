@@ -115,6 +115,51 @@ static int small_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st)
             : small_sweep_launch<T, IPMC_MODEL_LINEAR, false>(m, s, st);
 }
 
+// Speculation width for the small models (lanes per chain, small_spec_kernel):
+// lanes_per_chain if given (a power of two <= 64), else the widest that keeps
+// the ensemble within one wave per SIMD (1024 SIMDs x 64 lanes), when a launch
+// has more than one step to speculate over: wider groups waste more work after
+// the first acceptance and the machine turns throughput-bound (cfg 2, 4 096
+// chains, accept 5 %: width 16 = 299 M steps/s, 64 = 153 M, 1 = 67 M;
+// profiles/r1/spec_cfg2.txt).  -1: invalid request.
+static int small_spec_width(const ipmc_model& m, const ipmc_sweep& s) {
+  const int req = s.lanes_per_chain;
+  if (req > 0) {
+    if (req > 64 || (req & (req - 1))) return -1;
+    if (req > 1 && m.k > kSpecKMax) return -1;
+    return req;
+  }
+  int w = 1;
+  if (m.k <= kSpecKMax && s.n_steps > 1)
+    while (w < 64 && s.n_chains * (int64_t)w * 2 <= 65536) w *= 2;
+  return w;
+}
+
+template <typename T, int MODEL, bool FM>
+static int small_spec_launch(const ipmc_model& m, const ipmc_sweep& s, int w, hipStream_t st) {
+  const int64_t blocks = (s.n_chains * w + kSpecBlock - 1) / kSpecBlock;
+  switch (w) {
+#define IPMC_SPEC(W)                                                                                           \
+  case W:                                                                                                      \
+    hipLaunchKernelGGL((small_spec_kernel<T, MODEL, FM, W>), dim3((unsigned)blocks), dim3(kSpecBlock), 0, st, m, \
+                       s);                                                                                     \
+    return check_launch("small_spec_kernel");
+    IPMC_SPEC(2) IPMC_SPEC(4) IPMC_SPEC(8) IPMC_SPEC(16) IPMC_SPEC(32) IPMC_SPEC(64)
+#undef IPMC_SPEC
+  }
+  return fail(IPMC_ERR_UNSUPPORTED, "speculation width must be a power of two <= 64");
+}
+
+template <typename T>
+static int small_spec(const ipmc_model& m, const ipmc_sweep& s, int w, hipStream_t st) {
+  const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (m.kind == IPMC_MODEL_LORENZ63)
+    return fm ? small_spec_launch<T, IPMC_MODEL_LORENZ63, true>(m, s, w, st)
+              : small_spec_launch<T, IPMC_MODEL_LORENZ63, false>(m, s, w, st);
+  return fm ? small_spec_launch<T, IPMC_MODEL_LINEAR, true>(m, s, w, st)
+            : small_spec_launch<T, IPMC_MODEL_LINEAR, false>(m, s, w, st);
+}
+
 template <typename T, int MODEL, bool FM>
 static int small_eval_launch(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv,
                              void* out, bool phi, hipStream_t st) {
@@ -246,10 +291,15 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   switch (m->kind) {
     case IPMC_MODEL_LINEAR:
-    case IPMC_MODEL_LORENZ63:
-      if (s->lanes_per_chain > 1 || s->chains_per_lane > 1)
-        return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane");
+    case IPMC_MODEL_LORENZ63: {
+      if (s->chains_per_lane > 1) return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane group");
+      const int w = small_spec_width(*m, *s);
+      if (w < 0)
+        return fail(IPMC_ERR_UNSUPPORTED,
+                    "small models: lanes_per_chain (speculation width) must be a power of two <= 64, and 1 for k > 8");
+      if (w > 1) return s->dtype == IPMC_F64 ? small_spec<double>(*m, *s, w, st) : small_spec<float>(*m, *s, w, st);
       return s->dtype == IPMC_F64 ? small_sweep<double>(*m, *s, st) : small_sweep<float>(*m, *s, st);
+    }
     case IPMC_MODEL_LORENZ96: {
       int lpc, cpl;
       l96_layout(m->dim, s->dtype, s->n_chains, lpc, cpl);

@@ -156,6 +156,123 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
   }
 }
 
+// ------------------------------------------------------------ speculation
+// Small ensembles leave most of the GPU idle and a chain's steps are a
+// latency-bound sequence.  With S lanes per chain, lane s evaluates the step
+// st + s as if steps st .. st+s-1 were all rejected: its proposal is drawn
+// from the current state with the counter-based draws of step st + s, so it
+// is exactly the proposal the sequential chain makes if it gets there.  The
+// first lane whose proposal is accepted ends the round (later lanes' work is
+// discarded and redone from the new state), so u, Φ, the counters, the sums
+// and the samples are bit-identical to the one-lane kernel; a round advances
+// the chain by up to S steps in one forward-map latency.
+constexpr int kSpecBlock = 256;
+constexpr int kSpecKMax = 8;
+
+template <typename T, int MODEL, bool FM, int S>
+__global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model m, const ipmc_sweep s) {
+  __shared__ T vpark[kSpecKMax * kSpecBlock];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int sub = t & (S - 1);
+  const int gbase = lane & ~(S - 1);
+  const unsigned long long gmask = (S == 64) ? ~0ull : ((1ull << S) - 1);
+  const int64_t chain = ((int64_t)blockIdx.x * kSpecBlock + t) / S;
+  if (chain >= s.n_chains) return;  // whole groups leave together
+  const int k = m.k;
+  const uint64_t gid = (uint64_t)(s.chain_offset + chain);
+  T* __restrict__ u = (T*)s.u + chain * k;
+  const T* sq = (const T*)s.prior_sqrt;
+  const T* lo = (const T*)s.box_lo;
+  const T* hi = (const T*)s.box_hi;
+  const T* off = (const T*)s.box_off;
+  const T beta = (T)s.beta, contr = (T)s.contraction;
+  const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
+  T* phi = (T*)s.phi;
+  T* v = vpark + t;                       // this lane's proposal, v[j * kSpecBlock]
+  const T* vgroup = vpark + (t - sub);    // lane 0 of the group
+  T ur[kSpecKMax];
+#pragma unroll
+  for (int j = 0; j < kSpecKMax; ++j) ur[j] = j < k ? u[j] : (T)0;
+  T phu = phi[chain];
+  int64_t nacc = 0, ncalls = 0;
+  int64_t st = 0;
+  while (st < s.n_steps) {
+    const int64_t left = s.n_steps - st;
+    const int64_t tt = st + sub;
+    bool ok = false, acc = false;
+    T phv = (T)0;
+    if (sub < left) {
+      const uint64_t step = s.step0 + (uint64_t)tt;
+      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
+      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
+      double z0 = 0.0, z1 = 0.0;
+      ok = true;
+#pragma unroll
+      for (int j = 0; j < kSpecKMax; ++j) {
+        if (j < k) {
+          if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+          const T w = sq[j] * (T)((j & 1) ? z1 : z0);
+          const T vj = propose_one<T>(rw, ur[j], w, cs, bs);
+          v[j * kSpecBlock] = vj;
+          const T tb = vj + (off ? off[j] : (T)0);
+          if (lo && !(lo[j] < tb)) ok = false;
+          if (hi && !(tb < hi[j])) ok = false;
+        }
+      }
+      if (ok) {
+        phv = small_potential<T, MODEL, FM>(m, v, kSpecBlock, (const T*)s.y, (const T*)s.gamma_inv);
+        if (s.reg_scale) phv = phv + small_regularizer<T, FM>(k, (const T*)s.reg_scale, v, kSpecBlock);
+        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+      }
+    }
+    wave_sync_lds();
+    const unsigned long long accm = (__ballot(acc) >> gbase) & gmask;
+    const unsigned long long okm = (__ballot(ok) >> gbase) & gmask;
+    const int first = accm ? __builtin_ctzll(accm) : S;  // first accepted lane of the group
+    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
+    ncalls += __builtin_popcountll(okm & (used >= 64 ? ~0ull : ((1ull << used) - 1)));
+    const T phf = __shfl(phv, gbase + (first < S ? first : 0), 64);
+    if (s.sum_u && sub == 0) {
+      // the states after each of the `used` steps, in step order
+      for (int q = 0; q < used; ++q) {
+        const bool moved = (q == first);
+#pragma unroll
+        for (int j = 0; j < kSpecKMax; ++j) {
+          if (j < k) {
+            const double ud = moved ? (double)vgroup[j * kSpecBlock + first] : (double)ur[j];
+            s.sum_u[chain * k + j] += ud;
+            if (s.sum_u2) s.sum_u2[chain * k + j] += ud * ud;
+          }
+        }
+      }
+    }
+    if (first < S) {
+#pragma unroll
+      for (int j = 0; j < kSpecKMax; ++j)
+        if (j < k) ur[j] = vgroup[j * kSpecBlock + first];
+      phu = phf;
+      ++nacc;
+    }
+    wave_sync_lds();  // the parks are rewritten next round
+    st += used;
+  }
+  if (sub == 0) {
+    phi[chain] = phu;
+    if (s.accepts) s.accepts[chain] += nacc;
+    if (s.calls) s.calls[chain] += ncalls;
+#pragma unroll
+    for (int j = 0; j < kSpecKMax; ++j)
+      if (j < k) u[j] = ur[j];
+    if (s.sample_out) {
+      T* so = (T*)s.sample_out + chain * s.sample_stride;
+#pragma unroll
+      for (int j = 0; j < kSpecKMax; ++j)
+        if (j < k) so[j] = ur[j];
+    }
+  }
+}
+
 template <typename T, int MODEL, bool FM, bool PHI>
 __global__ __launch_bounds__(kSmallBlock) void small_eval_kernel(const ipmc_model m, int64_t n,
                                                                  const T* __restrict__ uin,

@@ -601,3 +601,37 @@ def test_burgers_every_layout_bit_exact(dev, orc):
             for lanes in lanes_list:
                 d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, torch.float64, dev, lanes=lanes)
                 _assert_same(d, o, (N, arith, lanes))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
+    """small_spec_kernel (S lanes evaluate S consecutive steps, the first
+    acceptance ends the round) equals the sequential chain bit for bit, for
+    every width, with schedules, box constraint, sums and the RW regularizer."""
+    from ip_mcmc_amd import LinearOperator, Lorenz63Operator
+
+    rng = np.random.default_rng(23)
+    ops = [LinearOperator(rng.normal(size=(3, 5)), rng.normal(size=5), arith="reference"),
+           Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=200),
+           Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=200, arith="reference")]
+    n = 37
+    sched = np.stack([np.linspace(0.05, 0.4, n), np.sqrt(1 - np.linspace(0.05, 0.4, n) ** 2)], axis=1)
+    for op in ops:
+        U0, phi0, y, ginv, sq = _problem(op, 45, dtype, orc, seed=2)
+        box = (np.full(op.k, -1.5), None, None)
+        for kw in (dict(), dict(box=box), dict(sched=sched), dict(want_sums=True)):
+            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, **kw)
+            assert 0 < o["acc"].sum() < 45 * n
+            for lanes in (1, 2, 8, 64):
+                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, dev, lanes=lanes, **kw)
+                _assert_same(d, o, (type(op).__name__, op.arith, lanes, list(kw)))
+                assert np.array_equal(d["samp"], o["u"])
+                if "want_sums" in kw:
+                    assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
+        rs = 0.5 + rng.random(op.k)
+        phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
+        o = _sweep_oracle(orc, op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, proposal="rw", reg_scale=rs)
+        for lanes in (4, 32):
+            d = _sweep_device(op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, dev, lanes=lanes, proposal="rw",
+                              reg_scale=rs)
+            _assert_same(d, o, (type(op).__name__, "rw", lanes))

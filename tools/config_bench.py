@@ -49,7 +49,7 @@ def make(cfg):
     raise SystemExit(f"unknown config {cfg}")
 
 
-def run(cfg, dtype, steps=3, lanes=0):
+def run(cfg, dtype, steps=3, lanes=0, per_launch=1):
     dev = torch.device("cuda", 0)
     op, n, beta, sq, flop, gamma = make(cfg)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
@@ -68,18 +68,18 @@ def run(cfg, dtype, steps=3, lanes=0):
     s.u, s.phi, s.accepts = u.data_ptr(), phi.data_ptr(), acc.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = y.data_ptr(), gi.data_ptr(), sqt.data_ptr()
     s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
-    s.seed, s.n_steps = 5, 1
+    s.seed, s.n_steps = 5, per_launch
     call("ipmc_pcn_sweep", C.byref(m), C.byref(s), st)  # warm-up
-    s.step0 = 1
+    s.step0 = per_launch
     torch.cuda.synchronize(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     for a, b in ev:
         a.record()
         call("ipmc_pcn_sweep", C.byref(m), C.byref(s), st)
         b.record()
-        s.step0 += 1
+        s.step0 += per_launch
     torch.cuda.synchronize(dev)
-    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) / per_launch
     res = {
         "config": cfg,
         "dtype": str(dtype).split(".")[-1],
@@ -87,8 +87,10 @@ def run(cfg, dtype, steps=3, lanes=0):
         "ms_per_sweep": ms,
         "pcn_steps_per_s": n / (ms * 1e-3),
         "tflops_algorithmic": n * flop / (ms * 1e-3) / 1e12,
-        "accept_rate": float(acc.sum().item()) / (n * (steps + 1)),
+        "accept_rate": float(acc.sum().item()) / (n * (steps + 1) * per_launch),
     }
+    if per_launch > 1:
+        res["steps_per_launch"] = per_launch
     if lanes:
         res["lanes_forced"] = lanes
     if isinstance(op, Lorenz96Operator):
@@ -98,7 +100,8 @@ def run(cfg, dtype, steps=3, lanes=0):
 
 if __name__ == "__main__":
     cfgs = sys.argv[1:] or ["cfg2", "cfg4", "cfg4full", "cfg4cfl", "cfg5"]
-    for c in cfgs:  # "cfg4:64" forces 64 lanes per chain
+    for c in cfgs:  # "cfg4:64" forces 64 lanes per chain, "cfg2@128" runs 128 pCN steps per launch
+        c, _, per = c.partition("@")
         name, _, lanes = c.partition(":")
         for dt in (torch.float64, torch.float32):
-            run(name, dt, lanes=int(lanes or 0))
+            run(name, dt, lanes=int(lanes or 0), per_launch=int(per or 1))
