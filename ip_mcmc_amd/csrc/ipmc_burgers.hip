@@ -229,12 +229,12 @@ __device__ T burgers_phi(const ipmc_model& m, const T (&v)[3], const BurCtx& c, 
     T acc = (T)0;
     for (int j = 0; j < m.q; ++j) {
       T gj = (T)__builtin_nan("");
-      if (valid) {
-        const int lo = m.win_lo[j], hi = m.win_hi[j];
-        int nt = hi - lo - 1;
-        if (nt < 0) nt = 0;
+      const int lo = m.win_lo[j], hi = m.win_hi[j];
+      int nt = hi - lo - 1;
+      if (nt < 0) nt = 0;
+      // a window outside [0, N) or wider than 129 cells is not measurable: G = NaN
+      if (valid && (nt == 0 || (lo >= 0 && lo + nt + 1 <= m.dim && nt <= 128)))
         gj = (T)m.meas_scale * trapz_pairwise<T>(row + lo, nt, mdxm);
-      }
       if (g_out) g_out[j] = gj;
       if (y) {
         const T r = (y[j] - gj) * ginv[j];

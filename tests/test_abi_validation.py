@@ -1,0 +1,172 @@
+"""The C-ABI's argument checks (include/ipmc.h), exercised on the CPU.
+
+Every call here fails validation (or is a no-op) before anything reaches the
+device, so no GPU is needed: the library returns the documented status code
+and ipmc_last_error() says why.  The pointers are dummies that are never
+dereferenced.  This is the boundary's equivalent of the reference's
+`assert 0 <= beta <= 1` (proposer.py:75) and ValueError paths.
+"""
+import ctypes as C
+
+import pytest
+
+from ip_mcmc_amd import _abi, _lib
+
+DUMMY = 0x10000  # a non-NULL "device pointer"; never dereferenced by these calls
+
+
+@pytest.fixture(scope="module")
+def h():
+    return _lib.lib()
+
+
+def _model(kind=_abi.MODEL_LORENZ96, k=40, q=40, dim=40, n_steps=10):
+    m = _abi.IpmcModel()
+    m.kind, m.arith, m.k, m.q, m.dim, m.n_steps, m.dt = kind, _abi.ARITH_FMA, k, q, dim, n_steps, 0.01
+    m.x0 = m.theta0 = m.A = DUMMY
+    return m
+
+
+def _sweep(n=8, k=40):
+    s = _abi.IpmcSweep()
+    s.dtype, s.n_chains, s.n_steps = _abi.F64, n, 1
+    s.u = s.phi = s.y = s.gamma_inv = s.prior_sqrt = DUMMY
+    s.beta, s.contraction = 0.5, 0.75 ** 0.5
+    return s
+
+
+def _status(h, rc, code, text):
+    assert rc == code, (rc, h.ipmc_last_error())
+    assert text in h.ipmc_last_error().decode()
+
+
+def test_model_checks(h):
+    sweep = C.byref(_sweep())
+    _status(h, h.ipmc_pcn_sweep(None, sweep, None), _abi.ERR_INVALID, "model is NULL")
+    m = _model(k=0)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "k and q must be positive")
+    m = _model()
+    m.theta0 = None
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "theta0 is NULL")
+    m = _model()
+    m.arith = 9
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "bad arith")
+    m = _model(kind=_abi.MODEL_LORENZ63, k=4, q=6)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "Lorenz-63")
+    m = _model(q=39)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "Lorenz-96")
+    m = _model(kind=_abi.MODEL_BURGERS, k=3, q=5, dim=256)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "Burgers")
+    m = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=29, dim=6)
+    m.fast_per_slow = 4
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_INVALID, "q == 5K")
+    m = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=5 * 65, dim=65)
+    m.fast_per_slow = 4
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_UNSUPPORTED, "K <= 64")
+    m = _model(kind=42)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_UNSUPPORTED, "unknown model kind")
+    m = _model(kind=_abi.MODEL_LINEAR, k=65, q=1)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), sweep, None), _abi.ERR_UNSUPPORTED, "k > 64")
+
+
+def test_sweep_checks(h):
+    m = C.byref(_model())
+    _status(h, h.ipmc_pcn_sweep(m, None, None), _abi.ERR_INVALID, "sweep is NULL")
+    s = _sweep()
+    s.dtype = 5
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "dtype")
+    s = _sweep()
+    s.proposal = 7
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "proposal")
+    for beta in (1.5, -0.1, float("nan")):
+        s = _sweep()
+        s.beta = beta
+        _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "beta has to be in [0,1]")
+    s = _sweep()
+    s.beta, s.proposal = 1.5, _abi.PROPOSAL_RW  # RW step sizes are not bounded by 1
+    s.u = None
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "is NULL")
+    s = _sweep(n=-1)
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "negative count")
+    s = _sweep()
+    s.sample_out, s.sample_stride = DUMMY, 39
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_stride < k")
+    s = _sweep()
+    s.sum_u2 = DUMMY
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sum_u2 needs sum_u")
+    # no chains or no steps: a no-op (nothing is launched)
+    assert h.ipmc_pcn_sweep(m, C.byref(_sweep(n=0)), None) == _abi.OK
+    s = _sweep()
+    s.n_steps = 0
+    assert h.ipmc_pcn_sweep(m, C.byref(s), None) == _abi.OK
+
+
+def test_layout_checks(h):
+    m = _model(dim=41, k=41, q=41)
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(_sweep(k=41)), None), _abi.ERR_UNSUPPORTED,
+            "no kernel compiled for dim=41")
+    m = _model()
+    s = _sweep()
+    s.lanes_per_chain = 16  # d=40 has no 16-lane instantiation
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "lanes_per_chain=16")
+    m = _model(kind=_abi.MODEL_LORENZ63, k=3, q=6, dim=3)
+    s = _sweep(k=3)
+    s.lanes_per_chain = 3
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "power of two")
+    s = _sweep(k=3)
+    s.chains_per_lane = 2
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "one chain per lane")
+    m = _model(kind=_abi.MODEL_BURGERS, k=3, q=5, dim=258)
+    m.n_windows, m.win_lo, m.win_hi = 5, DUMMY, DUMMY
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(_sweep(k=3)), None), _abi.ERR_UNSUPPORTED, "multiple of 4")
+
+
+def test_eval_and_rng_checks(h):
+    m = C.byref(_model())
+    _status(h, h.ipmc_forward(m, 7, 4, DUMMY, DUMMY, None), _abi.ERR_INVALID, "dtype")
+    _status(h, h.ipmc_forward(m, _abi.F64, -1, DUMMY, DUMMY, None), _abi.ERR_INVALID, "n must be >= 0")
+    _status(h, h.ipmc_forward(m, _abi.F64, 4, None, DUMMY, None), _abi.ERR_INVALID, "u / out is NULL")
+    _status(h, h.ipmc_potential(m, _abi.F64, 4, DUMMY, None, DUMMY, DUMMY, None), _abi.ERR_INVALID,
+            "y / gamma_inv is NULL")
+    assert h.ipmc_forward(m, _abi.F64, 0, None, None, None) == _abi.OK
+    _status(h, h.ipmc_normal(1, 0, -1, 0, 4, _abi.F64, DUMMY, None), _abi.ERR_INVALID, "negative count")
+    _status(h, h.ipmc_normal(1, 0, 4, 0, 4, 9, DUMMY, None), _abi.ERR_INVALID, "bad dtype")
+    _status(h, h.ipmc_uniform(1, 0, 4, 0, None, None), _abi.ERR_INVALID, "out is NULL")
+    assert h.ipmc_uniform(1, 0, 0, 0, None, None) == _abi.OK
+
+
+def test_diagnostics_checks(h):
+    _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, 1, 10, 10, 1, 11, DUMMY, None), _abi.ERR_INVALID,
+            "exceeds the series length")
+    _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, 1, 9000, 9000, 1, 10, DUMMY, None), _abi.ERR_UNSUPPORTED,
+            "longer than 8192")
+    _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, -1, 10, 10, 1, 5, DUMMY, None), _abi.ERR_INVALID, "negative")
+    assert h.ipmc_autocorr(None, _abi.F64, 0, 10, 10, 1, 5, None, None) == _abi.OK
+    _status(h, h.ipmc_burn_in(DUMMY, _abi.F64, 2, 3, 49, 147, 49, 1, 50, 0.03, DUMMY, DUMMY, None),
+            _abi.ERR_INVALID, "shorter than the window")
+    _status(h, h.ipmc_burn_in(DUMMY, 5, 2, 3, 60, 180, 60, 1, 50, 0.03, DUMMY, DUMMY, None), _abi.ERR_INVALID,
+            "bad dtype")
+    _status(h, h.ipmc_burn_in(DUMMY, _abi.F64, 2, 3, 60, 180, 60, 1, 50, 0.03, None, DUMMY, None),
+            _abi.ERR_INVALID, "NULL")
+    assert h.ipmc_burn_in(None, _abi.F64, 0, 3, 60, 180, 60, 1, 50, 0.03, None, None, None) == _abi.OK
+
+
+def test_auto_layout(h):
+    """The layout the sweep picks by itself: fp64 d=40 -> 4 lanes per
+    chain; fp32 -> two chains per lane group as f32x2, 4 lanes; d=256 -> 16 lanes."""
+    m = _model()
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 65536) == 104
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F32, 65536) == 204
+    assert h.ipmc_auto_lanes(C.byref(m), _abi.F64, 65536) == 4
+    m = _model(dim=256, k=256, q=256)
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 131072) == 116
+    assert h.ipmc_auto_layout(None, _abi.F64, 1) == 0
+
+
+def test_python_layer_raises_with_the_library_message():
+    from ip_mcmc_amd._lib import IpmcError, call
+
+    with pytest.raises(IpmcError, match="beta has to be in"):
+        s = _sweep()
+        s.beta = 2.0
+        call("ipmc_pcn_sweep", C.byref(_model()), C.byref(s), None)
