@@ -273,6 +273,7 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   if (s->proposal == IPMC_PROPOSAL_PCN && !(s->beta >= 0.0 && s->beta <= 1.0))
     return fail(IPMC_ERR_INVALID, "beta has to be in [0,1]");
   if (s->n_chains < 0 || s->n_steps < 0 || s->chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (s->n_steps > 0x7fffffff) return fail(IPMC_ERR_INVALID, "n_steps per launch must be < 2^31");
   if (s->n_chains == 0 || s->n_steps == 0) {
     if (s->n_chains > 0 && s->sample_out) {
       // no step: the sample is the current state

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
   T* phi = (T*)s.phi;
   T phu = phi[chain];
   const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
-  int64_t nacc = 0, ncalls = 0;
+  int nacc = 0, ncalls = 0;  // per launch (n_steps <= INT32_MAX, checked by the API)
   for (int64_t st = 0; st < s.n_steps; ++st) {
     const uint64_t step = s.step0 + (uint64_t)st;
     // Opaque per-step offset: keeps the loop-invariant per-component constants
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
   const V h = Splat<V>::of((float)m.dt);
   float* phi = (float*)s.phi;
   float pa = phi[ca], pb = phi[cb];
-  int64_t na = 0, nb = 0, ka = 0, kb = 0;
+  int na = 0, nb = 0, ka = 0, kb = 0;  // per launch (n_steps <= INT32_MAX)
   for (int64_t st = 0; st < s.n_steps; ++st) {
     const uint64_t step = s.step0 + (uint64_t)st;
     int cl = c0;

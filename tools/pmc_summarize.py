@@ -68,7 +68,8 @@ def main():
         if c in vals:
             rec[c] = mean(vals[c])
     if "GRBM_GUI_ACTIVE" in rec:
-        rec["effective_clock_GHz"] = rec["GRBM_GUI_ACTIVE"] / ns
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+        rec["effective_clock_GHz"] = rec["GRBM_GUI_ACTIVE"] / 8 / ns
     if "SQ_INSTS_VALU" in rec and "SQ_WAVES" in rec:
         rec["valu_instr_per_wave"] = rec["SQ_INSTS_VALU"] / rec["SQ_WAVES"]
     with open(out, "w") as f:

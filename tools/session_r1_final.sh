@@ -16,4 +16,5 @@ tools/gpu_session.sh \
   "fetch32:200:rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc32/fetch -o run -- $B32" \
   "write32:200:rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc32/write -o run -- $B32" \
   "sq32:200:rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc32/sq -o run -- $B32" \
-  "configs:400:python tools/config_bench.py cfg2 cfg4 cfg4full cfg4cfl cfg5 ts6 ts36 > gpurun_out/configs.jsonl"
+  "configs:400:python tools/config_bench.py cfg2 cfg2@128 cfg4 cfg4full cfg4cfl cfg5 ts6 ts36 > gpurun_out/configs.jsonl" \
+  "e2e:300:python tools/sampler_e2e.py 65536 20 5 > gpurun_out/sampler_e2e.jsonl"
