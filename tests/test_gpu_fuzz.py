@@ -1,0 +1,114 @@
+"""Seeded randomized parity: many small random problems through the C-ABI vs the oracle.
+
+Each case draws a model (linear, Lorenz-63, Lorenz-96 at a compiled dimension,
+two-scale Lorenz-96, Burgers), a dtype, an arithmetic mode, a layout (lanes per
+chain, chains per lane, speculation width), a ragged chain count, a chain
+offset and a step0 that crosses 2^32, the proposal (pCN or RW with a
+regularizer), an optional beta schedule, box constraint and running sums, and
+checks u, Φ, accepts, calls, samples and sums bit for bit.  The seed is fixed,
+so a failure is reproducible from its case number.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from test_gpu_parity import _assert_same, _np, _sweep_device, _sweep_oracle  # noqa: E402
+
+L96_DIMS = {4: (1, 2), 8: (1, 2, 4), 16: (1, 2, 4, 8), 20: (1, 2, 4), 32: (2, 4, 8, 16), 36: (2, 4),
+            40: (2, 4, 8), 64: (4, 8, 16), 128: (8, 16)}
+
+
+def _model(rng, case):
+    from ip_mcmc_amd import (BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator,
+                             TwoScaleLorenz96Operator)
+
+    arith = ["fma", "reference"][case % 2]
+    kind = ["linear", "l63", "l96", "l96", "ts", "burgers"][rng.integers(6)]
+    if kind == "linear":
+        k = int(rng.integers(1, 9))
+        return LinearOperator(rng.normal(size=(int(rng.integers(1, 6)), k)), rng.normal(size=k), arith=arith), {}
+    if kind == "l63":
+        return Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=int(rng.integers(5, 60)), arith=arith), {}
+    if kind == "l96":
+        d = int(rng.choice(list(L96_DIMS)))
+        x0 = 8.0 + rng.normal(size=d)
+        return Lorenz96Operator(d, 8.0, x0=x0, dt=0.005, n_steps=int(rng.integers(5, 40)), arith=arith), {"d": d}
+    if kind == "ts":
+        K, J = int(rng.integers(1, 12)), int(rng.choice([1, 2, 4, 8, 10, 16]))
+        x0 = rng.normal(size=K * (1 + J))
+        return TwoScaleLorenz96Operator(K=K, J=J, x0=x0, dt=0.004, n_steps=int(rng.integers(5, 30)),
+                                        moments=["reference", "mean"][rng.integers(2)], arith=arith), {}
+    N = int(rng.choice([32, 64, 128, 200, 256]))
+    mode = ["cfl", "fixed"][rng.integers(2)]
+    return BurgersOperator(N=N, dt_mode=mode, dt=2e-3, n_steps=int(rng.integers(20, 200)),
+                           T=float(rng.uniform(0.05, 0.3)), arith=arith), {"N": N}
+
+
+def _layout(rng, op, info, dtype):
+    from ip_mcmc_amd import BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator
+
+    if isinstance(op, Lorenz96Operator):
+        d = info["d"]
+        opts = [lp for lp in L96_DIMS[d] if (d // lp) * 8 <= 160]
+        lanes = int(rng.choice(opts)) if opts else 0
+        cpl = 2 if (dtype == torch.float32 and rng.random() < 0.5) else 1
+        return lanes, cpl
+    if isinstance(op, BurgersOperator):
+        N = info["N"]
+        opts = [lp for lp in (16, 32, 64) if N % lp == 0 and N // lp in (4, 8)]
+        return (int(rng.choice(opts)) if opts and rng.random() < 0.5 else 0), 0
+    if isinstance(op, (LinearOperator, Lorenz63Operator)) and op.k <= 8:
+        return int(rng.choice([0, 1, 2, 4, 16, 64])), 0
+    return 0, 0
+
+
+@pytest.mark.parametrize("case", range(120))
+def test_random_sweeps_bit_exact(dev_fuzz, orc, case):
+    rng = np.random.default_rng(1000 + case)
+    op, info = _model(rng, case)
+    dtype = [torch.float64, torch.float32][rng.integers(2)]
+    lanes, cpl = _layout(rng, op, info, dtype)
+    C = int(rng.integers(1, 140))
+    k = op.k
+    U0 = (0.2 * rng.normal(size=(C, k))).astype(_np(dtype)).astype(np.float64)
+    g = orc.forward(op, 0.1 * rng.normal(size=(1, k)))[0]
+    y = np.nan_to_num(g) + 0.05 * rng.normal(size=op.q)
+    ginv = 1.0 / rng.uniform(0.03, 0.3, size=op.q)
+    sq = rng.uniform(0.3, 1.5, size=k)
+    n = int(rng.integers(1, 7))
+    kw = {}
+    proposal = "rw" if rng.random() < 0.3 else "pcn"
+    beta = float(rng.uniform(0.05, 0.6))
+    reg = None
+    if proposal == "rw":
+        reg = rng.uniform(0.5, 2.0, size=k)
+        phi0 = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=reg).astype(np.float64)
+    else:
+        phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
+    if rng.random() < 0.3:
+        b = rng.uniform(0.05, 0.5, size=n)
+        kw["sched"] = np.stack([b, np.sqrt(1 - b**2) if proposal == "pcn" else np.ones(n)], axis=1)
+    if rng.random() < 0.3:
+        kw["box"] = (np.full(k, -0.35), None, None)
+    if rng.random() < 0.3:
+        kw["want_sums"] = True
+    seed = int(rng.integers(0, 2**63))
+    step0 = int(rng.integers(0, 2**34))
+    offset = int(rng.integers(0, 2**31))
+    o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n, dtype, chain_offset=offset,
+                      proposal=proposal, reg_scale=reg, **kw)
+    d = _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n, dtype, dev_fuzz, lanes=lanes, cpl=cpl,
+                      chain_offset=offset, proposal=proposal, reg_scale=reg, **kw)
+    what = (case, type(op).__name__, op.arith, str(dtype), lanes, cpl, C, n, proposal, sorted(kw))
+    _assert_same(d, o, what)
+    assert np.array_equal(d["samp"], o["u"]), what
+    if kw.get("want_sums"):
+        assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"]), what
+
+
+@pytest.fixture(scope="module")
+def dev_fuzz():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return torch.device("cuda", 0)
