@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 4
+#define IPMC_ABI_VERSION 5
 
 typedef enum {
   IPMC_OK = 0,
@@ -117,7 +117,10 @@ typedef struct ipmc_sweep {
   int32_t dtype;            /* ipmc_dtype of u/phi/y/gamma_inv/prior_sqrt/box_* */
   int32_t lanes_per_chain;  /* 0 = auto; otherwise a divisor of the state dim (kernel layout only: results are identical) */
   int32_t chains_per_lane;  /* 0 = auto; 2 = two fp32 chains packed per lane group (v_pk_*_f32), 1 = one (layout only) */
-  int32_t reserved0;
+  int32_t spec_width;       /* speculative steps per round (0 = auto, 1 = off; a power of two): spec_width lane
+                               groups per chain each evaluate one of the next steps from the current state, the
+                               first acceptance ends the round -- results identical, small ensembles run faster.
+                               Lorenz-63 / linear (k <= 8) and Lorenz-96 (spec_width * lanes_per_chain <= 64). */
   int64_t n_chains;
   int64_t chain_offset;     /* global id of chain 0 of this shard (RNG counter) */
   void* u;                  /* [n_chains, k] in/out current state */

@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -56,7 +56,7 @@ class IpmcSweep(C.Structure):
         ("dtype", C.c_int32),
         ("lanes_per_chain", C.c_int32),
         ("chains_per_lane", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("spec_width", C.c_int32),
         ("n_chains", C.c_int64),
         ("chain_offset", C.c_int64),
         ("u", C.c_void_p),

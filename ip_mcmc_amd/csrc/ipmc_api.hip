@@ -116,14 +116,14 @@ static int small_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st)
 }
 
 // Speculation width for the small models (lanes per chain, small_spec_kernel):
-// lanes_per_chain if given (a power of two <= 64), else the widest that keeps
+// spec_width if given (a power of two <= 64), else the widest that keeps
 // the ensemble within one wave per SIMD (1024 SIMDs x 64 lanes), when a launch
 // has more than one step to speculate over: wider groups waste more work after
 // the first acceptance and the machine turns throughput-bound (cfg 2, 4 096
 // chains, accept 5 %: width 16 = 299 M steps/s, 64 = 153 M, 1 = 67 M;
 // profiles/r1/spec_cfg2.txt).  -1: invalid request.
 static int small_spec_width(const ipmc_model& m, const ipmc_sweep& s) {
-  const int req = s.lanes_per_chain;
+  const int req = s.spec_width;
   if (req > 0) {
     if (req > 64 || (req & (req - 1))) return -1;
     if (req > 1 && m.k > kSpecKMax) return -1;
@@ -293,11 +293,11 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   switch (m->kind) {
     case IPMC_MODEL_LINEAR:
     case IPMC_MODEL_LORENZ63: {
-      if (s->chains_per_lane > 1) return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane group");
+      if (s->chains_per_lane > 1 || s->lanes_per_chain > 1)
+        return fail(IPMC_ERR_UNSUPPORTED, "small models run one chain per lane (spec_width adds speculative lanes)");
       const int w = small_spec_width(*m, *s);
       if (w < 0)
-        return fail(IPMC_ERR_UNSUPPORTED,
-                    "small models: lanes_per_chain (speculation width) must be a power of two <= 64, and 1 for k > 8");
+        return fail(IPMC_ERR_UNSUPPORTED, "small models: spec_width must be a power of two <= 64, and 1 for k > 8");
       if (w > 1) return s->dtype == IPMC_F64 ? small_spec<double>(*m, *s, w, st) : small_spec<float>(*m, *s, w, st);
       return s->dtype == IPMC_F64 ? small_sweep<double>(*m, *s, st) : small_sweep<float>(*m, *s, st);
     }
@@ -310,7 +310,26 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
         set_error("Lorenz-96: no kernel compiled for dim=%d lanes_per_chain=%d chains_per_lane=%d", m->dim, lpc, cpl);
         return IPMC_ERR_UNSUPPORTED;
       }
-      return s->dtype == IPMC_F64 ? l96_sweep_f64(*m, *s, lpc, st) : l96_sweep_f32(*m, *s, lpc, cpl, st);
+      // speculation (l96_spec_kernel): spec_width slots of lpc lanes per chain,
+      // auto = the widest keeping the ensemble within one wave per SIMD
+      int spec = s->spec_width;
+      if (spec < 0 || spec > 64 || (spec & (spec - 1)))
+        return fail(IPMC_ERR_UNSUPPORTED, "spec_width must be a power of two <= 64");
+      if (spec == 0) {
+        spec = 1;
+        if (s->n_steps > 1 && s->chains_per_lane != 2)
+          while (spec * 2 * lpc <= 64 && s->n_chains * (int64_t)lpc * spec * 2 <= 65536) spec *= 2;
+      }
+      if (spec > 1) {
+        if (spec * lpc > 64) return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: spec_width * lanes_per_chain must be <= 64");
+        if (cpl == 2) {
+          if (s->chains_per_lane == 2)
+            return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: speculation runs one chain per lane group");
+          cpl = 1;  // the packed fp32 layout is for full ensembles; fp32 one-chain kernels speculate
+        }
+      }
+      return s->dtype == IPMC_F64 ? l96_sweep_f64(*m, *s, lpc, spec, st)
+                                  : l96_sweep_f32(*m, *s, lpc, cpl, spec, st);
     }
     case IPMC_MODEL_BURGERS:
       return burgers_sweep(*m, *s, st);

@@ -12,8 +12,9 @@ int check_launch(const char* what);
 
 // Lorenz-96 dispatch (ipmc_l96_f32.hip / ipmc_l96_f64.hip).
 // Returns IPMC_ERR_UNSUPPORTED when (D, lpc) has no instantiation.
-int l96_sweep_f32(const ipmc_model& m, const ipmc_sweep& s, int lpc, int cpl, hipStream_t st);
-int l96_sweep_f64(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st);
+// spec > 1: speculative sweep with `spec` slots per chain (one chain per lane group only).
+int l96_sweep_f32(const ipmc_model& m, const ipmc_sweep& s, int lpc, int cpl, int spec, hipStream_t st);
+int l96_sweep_f64(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hipStream_t st);
 int l96_eval_f32(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
                  int lpc, hipStream_t st);
 int l96_eval_f64(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,

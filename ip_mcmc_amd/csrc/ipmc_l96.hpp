@@ -206,6 +206,113 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
   }
 }
 
+// Speculative sweep for ensembles too small to fill the GPU (as
+// small_spec_kernel, ipmc_small.hpp): S slots of LPC lanes per chain
+// (S*LPC <= 64, one wavefront); slot s evaluates step st+s from the current
+// state -- exactly the proposal the sequential chain makes there if steps
+// st .. st+s-1 are rejected -- and the first accepting slot ends the round.
+// The state lives in registers of every slot (ur) and moves through the LDS
+// park on acceptance.  Bit-identical to l96_sweep_kernel.
+template <typename T, int D, int LPC, bool FM>
+__global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
+  constexpr int M = D / LPC;
+  __shared__ T vpark[M][kL96Block];
+  __shared__ T stage[l96_stage_len<M, LPC>()];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int G = S * LPC;  // lanes per chain (a power of two <= 64)
+  const int64_t tid = (int64_t)blockIdx.x * kL96Block + t;
+  const int64_t chain = tid / G;
+  const int r = (int)(tid % G);
+  const int slot = r / LPC, sub = r % LPC;
+  const int gbase = lane - r;  // the chain's first lane in the wavefront
+  if (chain >= s.n_chains) return;
+  const uint64_t gid = (uint64_t)(s.chain_offset + chain);
+  const int c0 = sub * M;
+  T* __restrict__ u = (T*)s.u + chain * D + c0;
+  const T beta = (T)s.beta, contr = (T)s.contraction, h = (T)m.dt;
+  T* phi = (T*)s.phi;
+  T ur[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) ur[j] = u[j];
+  T phu = phi[chain];
+  const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
+  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
+  int nacc = 0, ncalls = 0;
+  int64_t st = 0;
+  while (st < s.n_steps) {
+    const int64_t left = s.n_steps - st;
+    const int64_t tt = st + slot;
+    bool ok = false, acc = false;
+    T phv = (T)0;
+    int cl = c0;
+    asm volatile("" : "+v"(cl));
+    if (slot < left) {  // uniform per slot
+      const uint64_t step = s.step0 + (uint64_t)tt;
+      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
+      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
+      T v[M];
+      pcn_propose<T, M>(ur, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw);
+#pragma unroll
+      for (int j = 0; j < M; ++j) vpark[j][t] = v[j];
+      ok = box_valid<T, M, LPC>(s, c0, v, lane);
+      if (ok) {
+        const T reg = s.reg_scale
+                          ? regularizer<T, M, LPC, FM, T, kL96Block>((const T*)s.reg_scale + cl, v, lane, stage)
+                          : (T)0;
+        phv = l96_potential<T, M, LPC, FM>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
+                                           (const T*)s.gamma_inv + cl, h, m.n_steps, lane, stage);
+        if (s.reg_scale) phv = phv + reg;
+        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+      }
+    }
+    wave_sync_lds();
+    // one bit per slot: the slot's lane sub == 0, at bit slot*LPC
+    const unsigned long long accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
+    const unsigned long long okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
+    const int first = accm ? __builtin_ctzll(accm) / LPC : S;
+    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
+    const int ubits = used * LPC;
+    ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+    const T phf = __shfl(phv, gbase + (first < S ? first : 0) * LPC, 64);
+    const int win = t - r + (first < S ? first : 0) * LPC + sub;  // the winning slot's lane for my components
+    if (s.sum_u && slot == 0) {
+      double* su = s.sum_u + chain * D + c0;
+      double* su2 = s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr;
+      for (int q = 0; q < used; ++q) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const double ud = (q == first) ? (double)vpark[j][win] : (double)ur[j];
+          su[j] += ud;
+          if (su2) su2[j] += ud * ud;
+        }
+      }
+    }
+    if (first < S) {
+#pragma unroll
+      for (int j = 0; j < M; ++j) ur[j] = vpark[j][win];
+      phu = phf;
+      ++nacc;
+    }
+    wave_sync_lds();  // the parks are rewritten next round
+    st += used;
+  }
+  if (slot == 0) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) u[j] = ur[j];
+    if (sub == 0) {
+      phi[chain] = phu;
+      if (s.accepts) s.accepts[chain] += nacc;
+      if (s.calls) s.calls[chain] += ncalls;
+    }
+    if (s.sample_out) {
+      T* so = (T*)s.sample_out + chain * s.sample_stride + c0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) so[j] = ur[j];
+    }
+  }
+}
+
 // fp32, two chains per lane group (x = chain 2p, y = chain 2p+1): the RK loop
 // runs on f32x2 so every FLOP is a v_pk_*_f32; proposal and accept stay per
 // chain (scalar), so the bits equal the one-chain kernel's.

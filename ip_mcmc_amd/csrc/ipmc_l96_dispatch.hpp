@@ -17,8 +17,15 @@ constexpr bool l96_ok() {
   return LPC <= 16 && D % LPC == 0 && D / LPC >= 2 && (D / LPC) * (int)sizeof(T) <= 160;
 }
 
+// spec > 1: the speculative kernel with spec slots of LPC lanes per chain.
 template <typename T, int D, int LPC, bool FM>
-int l96_launch_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
+int l96_launch_sweep(const ipmc_model& m, const ipmc_sweep& s, int spec, hipStream_t st) {
+  if (spec > 1) {
+    const int64_t blocks = (s.n_chains * LPC * spec + kL96Block - 1) / kL96Block;
+    hipLaunchKernelGGL((l96_spec_kernel<T, D, LPC, FM>), dim3((unsigned)blocks), dim3(kL96Block), 0, st, m, s,
+                       spec);
+    return check_launch("l96_spec_kernel");
+  }
   const int64_t threads = s.n_chains * LPC;
   const int64_t blocks = (threads + kL96Block - 1) / kL96Block;
   hipLaunchKernelGGL((l96_sweep_kernel<T, D, LPC, FM>), dim3((unsigned)blocks), dim3(kL96Block), 0, st, m, s);
@@ -40,11 +47,11 @@ int l96_launch_eval(const ipmc_model& m, int64_t n, const void* u, const void* y
 }
 
 template <typename T, int D, bool FM>
-int l96_sweep_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+int l96_sweep_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hipStream_t st) {
   switch (lpc) {
-#define IPMC_CASE(L)                                                                   \
-  case L:                                                                              \
-    if constexpr (l96_ok<T, D, L>()) return l96_launch_sweep<T, D, L, FM>(m, s, st); \
+#define IPMC_CASE(L)                                                                         \
+  case L:                                                                                    \
+    if constexpr (l96_ok<T, D, L>()) return l96_launch_sweep<T, D, L, FM>(m, s, spec, st); \
     break;
     IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
 #undef IPMC_CASE
@@ -100,11 +107,12 @@ int l96_eval_d(const ipmc_model& m, int64_t n, const void* u, const void* y, con
 }
 
 template <typename T>
-int l96_sweep_t(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
+int l96_sweep_t(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hipStream_t st) {
   const bool fm = (m.arith == IPMC_ARITH_FMA);
   switch (m.dim) {
-#define IPMC_DIM(D) \
-  case D: return fm ? l96_sweep_d<T, D, true>(m, s, lpc, st) : l96_sweep_d<T, D, false>(m, s, lpc, st);
+#define IPMC_DIM(D)                                                                 \
+  case D:                                                                           \
+    return fm ? l96_sweep_d<T, D, true>(m, s, lpc, spec, st) : l96_sweep_d<T, D, false>(m, s, lpc, spec, st);
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }

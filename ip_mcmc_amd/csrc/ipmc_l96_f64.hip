@@ -3,8 +3,8 @@
 
 namespace ipmc {
 
-int l96_sweep_f64(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
-  return l96_sweep_t<double>(m, s, lpc, st);
+int l96_sweep_f64(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hipStream_t st) {
+  return l96_sweep_t<double>(m, s, lpc, spec, st);
 }
 int l96_eval_f64(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
                  int lpc, hipStream_t st) {

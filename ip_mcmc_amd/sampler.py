@@ -120,7 +120,13 @@ class MCMCSampler:
         lanes_per_chain=0,
         chain_offset=0,
         verbose=False,
+        spec_width=0,
     ):
+        """Reference signature (sampler.py:7-10) plus device options:
+        dtype (np.float64 or np.float32), device, lanes_per_chain (kernel
+        layout, 0 = auto), chain_offset (global id of chain 0, for sharding),
+        spec_width (speculative steps per round for small ensembles: 0 = auto,
+        1 = off; results are identical either way)."""
         self.proposer = proposal
         self.accepter = acceptance
         self.rng = rng
@@ -129,6 +135,7 @@ class MCMCSampler:
         self.lanes_per_chain = int(lanes_per_chain)
         self.chain_offset = int(chain_offset)
         self.verbose = verbose
+        self.spec_width = int(spec_width)
         # state of the last run (device tensors), for inspection / continuation
         self.state = None
         self.last_run_seconds = None
@@ -202,6 +209,7 @@ class MCMCSampler:
         sw = _abi.IpmcSweep()
         sw.dtype = dev.abi_dtype(td)
         sw.lanes_per_chain = self.lanes_per_chain
+        sw.spec_width = self.spec_width
         sw.n_chains = n_chains
         sw.chain_offset = self.chain_offset
         sw.u = U.data_ptr()

@@ -111,11 +111,21 @@ def test_layout_checks(h):
     _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "lanes_per_chain=16")
     m = _model(kind=_abi.MODEL_LORENZ63, k=3, q=6, dim=3)
     s = _sweep(k=3)
-    s.lanes_per_chain = 3
+    s.spec_width = 3
     _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "power of two")
     s = _sweep(k=3)
     s.chains_per_lane = 2
     _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "one chain per lane")
+    s = _sweep(k=3)
+    s.lanes_per_chain = 4
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "one chain per lane")
+    m = _model()
+    s = _sweep()
+    s.lanes_per_chain, s.spec_width = 8, 16  # 128 lanes per chain > one wavefront
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "<= 64")
+    s = _sweep()
+    s.chains_per_lane, s.spec_width, s.dtype = 2, 4, _abi.F32
+    _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(s), None), _abi.ERR_UNSUPPORTED, "one chain per lane group")
     m = _model(kind=_abi.MODEL_BURGERS, k=3, q=5, dim=258)
     m.n_windows, m.win_lo, m.win_hi = 5, DUMMY, DUMMY
     _status(h, h.ipmc_pcn_sweep(C.byref(m), C.byref(_sweep(k=3)), None), _abi.ERR_UNSUPPORTED, "multiple of 4")

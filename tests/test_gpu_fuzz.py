@@ -54,14 +54,15 @@ def _layout(rng, op, info, dtype):
         opts = [lp for lp in L96_DIMS[d] if (d // lp) * 8 <= 160]
         lanes = int(rng.choice(opts)) if opts else 0
         cpl = 2 if (dtype == torch.float32 and rng.random() < 0.5) else 1
-        return lanes, cpl
+        spec = 1 if cpl == 2 else int(rng.choice([w for w in (0, 1, 2, 4, 8, 16, 32, 64) if w * lanes <= 64]))
+        return lanes, cpl, spec
     if isinstance(op, BurgersOperator):
         N = info["N"]
         opts = [lp for lp in (16, 32, 64) if N % lp == 0 and N // lp in (4, 8)]
-        return (int(rng.choice(opts)) if opts and rng.random() < 0.5 else 0), 0
+        return (int(rng.choice(opts)) if opts and rng.random() < 0.5 else 0), 0, 1
     if isinstance(op, (LinearOperator, Lorenz63Operator)) and op.k <= 8:
-        return int(rng.choice([0, 1, 2, 4, 16, 64])), 0
-    return 0, 0
+        return 0, 0, int(rng.choice([0, 1, 2, 4, 16, 64]))
+    return 0, 0, 1
 
 
 @pytest.mark.parametrize("case", range(120))
@@ -69,7 +70,7 @@ def test_random_sweeps_bit_exact(dev_fuzz, orc, case):
     rng = np.random.default_rng(1000 + case)
     op, info = _model(rng, case)
     dtype = [torch.float64, torch.float32][rng.integers(2)]
-    lanes, cpl = _layout(rng, op, info, dtype)
+    lanes, cpl, spec = _layout(rng, op, info, dtype)
     C = int(rng.integers(1, 140))
     k = op.k
     U0 = (0.2 * rng.normal(size=(C, k))).astype(_np(dtype)).astype(np.float64)
@@ -100,8 +101,8 @@ def test_random_sweeps_bit_exact(dev_fuzz, orc, case):
     o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n, dtype, chain_offset=offset,
                       proposal=proposal, reg_scale=reg, **kw)
     d = _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n, dtype, dev_fuzz, lanes=lanes, cpl=cpl,
-                      chain_offset=offset, proposal=proposal, reg_scale=reg, **kw)
-    what = (case, type(op).__name__, op.arith, str(dtype), lanes, cpl, C, n, proposal, sorted(kw))
+                      chain_offset=offset, proposal=proposal, reg_scale=reg, spec=spec, **kw)
+    what = (case, type(op).__name__, op.arith, str(dtype), lanes, cpl, spec, C, n, proposal, sorted(kw))
     _assert_same(d, o, what)
     assert np.array_equal(d["samp"], o["u"]), what
     if kw.get("want_sums"):

@@ -86,7 +86,9 @@ def test_forward_and_potential_bit_exact(dev, orc, dtype):
 
 # ----------------------------------------------------------------- sweep
 def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, dev, lanes=0, box=None,
-                  sched=None, chain_offset=0, want_sums=False, cpl=0, proposal="pcn", reg_scale=None):
+                  sched=None, chain_offset=0, want_sums=False, cpl=0, proposal="pcn", reg_scale=None, spec=1):
+    """One ipmc_pcn_sweep launch.  spec=1 (default) runs the sequential kernels;
+    spec=0 lets the library choose a speculation width, >1 forces one."""
     from ip_mcmc_amd import _abi
     from ip_mcmc_amd._lib import call
 
@@ -102,6 +104,7 @@ def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, 
     s.dtype = _abi.F64 if dtype == torch.float64 else _abi.F32
     s.lanes_per_chain = lanes
     s.chains_per_lane = cpl
+    s.spec_width = spec
     s.n_chains, s.chain_offset = U.shape[0], chain_offset
     s.u, s.phi, s.accepts, s.calls = U.data_ptr(), phi.data_ptr(), acc.data_ptr(), calls.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = yt.data_ptr(), gt.data_ptr(), st.data_ptr()
@@ -622,16 +625,50 @@ def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
         for kw in (dict(), dict(box=box), dict(sched=sched), dict(want_sums=True)):
             o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, **kw)
             assert 0 < o["acc"].sum() < 45 * n
-            for lanes in (1, 2, 8, 64):
-                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, dev, lanes=lanes, **kw)
-                _assert_same(d, o, (type(op).__name__, op.arith, lanes, list(kw)))
+            for w in (1, 0, 2, 8, 64):
+                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, dev, spec=w, **kw)
+                _assert_same(d, o, (type(op).__name__, op.arith, w, list(kw)))
                 assert np.array_equal(d["samp"], o["u"])
                 if "want_sums" in kw:
                     assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
         rs = 0.5 + rng.random(op.k)
         phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
         o = _sweep_oracle(orc, op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, proposal="rw", reg_scale=rs)
-        for lanes in (4, 32):
-            d = _sweep_device(op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, dev, lanes=lanes, proposal="rw",
+        for w in (4, 32):
+            d = _sweep_device(op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, dev, spec=w, proposal="rw",
                               reg_scale=rs)
-            _assert_same(d, o, (type(op).__name__, "rw", lanes))
+            _assert_same(d, o, (type(op).__name__, "rw", w))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_l96_speculative_sweeps_bit_exact(dev, orc, dtype):
+    """l96_spec_kernel (spec_width slots of lanes_per_chain lanes per chain) equals the
+    sequential chain bit for bit, for every (lanes, width) pair, with schedules,
+    box constraint, sums, the RW regularizer and both arithmetic modes."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    n = 23
+    sched = np.stack([np.linspace(0.05, 0.4, n), np.sqrt(1 - np.linspace(0.05, 0.4, n) ** 2)], axis=1)
+    for K, lanes_list, arith in ((8, (1, 2, 4), "fma"), (40, (2, 4, 8), "fma"), (32, (4, 16), "reference")):
+        op = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=40, arith=arith)
+        U0, phi0, y, ginv, sq = _problem(op, 21, dtype, orc, seed=K)
+        ginv = ginv * 0.05  # a broad posterior: acceptances happen inside the rounds
+        phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
+        box = (np.full(K, -0.6), None, None)
+        for kw in (dict(), dict(box=box, sched=sched), dict(want_sums=True)):
+            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 5, 2**32 - 7, n, dtype, **kw)
+            assert 0 < o["acc"].sum() < 21 * n, o["acc"].sum()
+            for lanes in lanes_list:
+                for w in (0, 2, 64 // lanes):
+                    d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 5, 2**32 - 7, n, dtype, dev, lanes=lanes,
+                                      cpl=1, spec=w, **kw)
+                    _assert_same(d, o, (K, arith, lanes, w, list(kw)))
+                    assert np.array_equal(d["samp"], o["u"])
+                    if "want_sums" in kw:
+                        assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
+        rs = np.linspace(0.5, 2.0, K)
+        phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
+        o = _sweep_oracle(orc, op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, proposal="rw", reg_scale=rs)
+        d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, lanes=lanes_list[-1], cpl=1,
+                          spec=4, proposal="rw", reg_scale=rs)
+        _assert_same(d, o, (K, "rw"))

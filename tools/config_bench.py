@@ -7,6 +7,7 @@ cfg4     Burgers N=256, fixed dt 1e-3 x 1000, 2 048 chains (= 16 384 / 8 GPUs)
 cfg4full Burgers as cfg4 with all 16 384 chains on one GPU
 cfg4cfl  Burgers N=256, reference CFL time stepping, 2 048 chains
 cfg5     Lorenz-96 d=256, 10 000 RK4 steps, 131 072 chains (= 2^20 / 8 GPUs)
+l96xN    the headline problem with N = 1, 64 or 1024 chains (speculative sweeps)
 ts6      two-scale Lorenz-96 K=6 J=4 (the thesis problem, lorenz_mcmc.py:87-88), T=20 (4 000 RK4 steps), 65 536 chains
 ts36     two-scale Lorenz-96 K=36 J=10, 2 000 RK4 steps of 0.002, 16 384 chains
 """
@@ -46,10 +47,14 @@ def make(cfg):
     if cfg == "ts36":
         op = TwoScaleLorenz96Operator(K=36, J=10, dt=0.002, n_steps=2000, moments="mean")
         return op, 16384, 0.5, np.sqrt([10.0, 1.0, 10.0]), 45 * 396 * 2000, 0.5
+    if cfg in ("l96x1", "l96x64", "l96x1024"):
+        # the headline problem with few chains (the reference runs one): speculation territory
+        op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=2000)
+        return op, int(cfg[4:]), 0.2, np.ones(40), 30 * 40 * 2000, 0.1
     raise SystemExit(f"unknown config {cfg}")
 
 
-def run(cfg, dtype, steps=3, lanes=0, per_launch=1):
+def run(cfg, dtype, steps=3, lanes=0, per_launch=1, spec=None):
     dev = torch.device("cuda", 0)
     op, n, beta, sq, flop, gamma = make(cfg)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
@@ -64,7 +69,13 @@ def run(cfg, dtype, steps=3, lanes=0, per_launch=1):
     call("ipmc_potential", C.byref(m), adt, n, u.data_ptr(), y.data_ptr(), gi.data_ptr(), phi.data_ptr(), st)
     acc = torch.zeros(n, dtype=torch.int64, device=dev)
     s = _abi.IpmcSweep()
-    s.dtype, s.n_chains, s.lanes_per_chain = adt, n, lanes
+    s.dtype, s.n_chains = adt, n
+    if isinstance(op, (Lorenz63Operator,)):
+        s.spec_width = lanes  # small models: the ":" option is the speculation width
+    else:
+        s.lanes_per_chain = lanes
+    if spec is not None:
+        s.spec_width = spec
     s.u, s.phi, s.accepts = u.data_ptr(), phi.data_ptr(), acc.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = y.data_ptr(), gi.data_ptr(), sqt.data_ptr()
     s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
@@ -93,6 +104,8 @@ def run(cfg, dtype, steps=3, lanes=0, per_launch=1):
         res["steps_per_launch"] = per_launch
     if lanes:
         res["lanes_forced"] = lanes
+    if spec is not None:
+        res["spec_width"] = spec
     if isinstance(op, Lorenz96Operator):
         res["lanes_per_chain"] = lib().ipmc_auto_lanes(C.byref(m), adt, n)
     print(json.dumps(res), flush=True)
@@ -100,8 +113,12 @@ def run(cfg, dtype, steps=3, lanes=0, per_launch=1):
 
 if __name__ == "__main__":
     cfgs = sys.argv[1:] or ["cfg2", "cfg4", "cfg4full", "cfg4cfl", "cfg5"]
-    for c in cfgs:  # "cfg4:64" forces 64 lanes per chain, "cfg2@128" runs 128 pCN steps per launch
-        c, _, per = c.partition("@")
-        name, _, lanes = c.partition(":")
+    # "cfg4:64" forces 64 lanes per chain (small models: speculation width), "cfg2@128" runs
+    # 128 pCN steps per launch, "l96x1~1" sets spec_width 1 (no speculation)
+    import re
+
+    for c in cfgs:
+        name = re.match(r"[a-z0-9]+", c).group(0)
+        opt = {k: int(v) for k, v in re.findall(r"([:@~])(\d+)", c)}
         for dt in (torch.float64, torch.float32):
-            run(name, dt, lanes=int(lanes or 0), per_launch=int(per or 1))
+            run(name, dt, lanes=opt.get(":", 0), per_launch=opt.get("@", 1), spec=opt.get("~"))
