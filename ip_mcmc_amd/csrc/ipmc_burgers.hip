@@ -249,63 +249,94 @@ __device__ T burgers_phi(const ipmc_model& m, const T (&v)[3], const BurCtx& c, 
 
 constexpr int kBurQMax = 64;
 
+// S speculative slots of GS lanes per chain (S = 1: the sequential chain; S·GS
+// <= 64): slot s evaluates step st+s from the current state as if the steps
+// before it in the round were rejected; the first accepting slot ends the
+// round (see small_spec_kernel) -- bit-identical to S = 1.
 template <typename T, int CPL, int GS, bool FM>
-__global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
+__global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
   __shared__ T lds[kBurBlock * CPL];
   const int lane = threadIdx.x & 63;
+  const int G = S * GS;
   const int64_t tid = (int64_t)blockIdx.x * kBurBlock + threadIdx.x;
-  const int64_t chain = tid / GS;
-  const BurCtx c{(int)(tid % GS), lane, m.dim / CPL};
+  const int64_t chain = tid / G;
+  const int r = (int)(tid % G);
+  const int slot = r / GS;
+  const int cbase = lane - r;
+  const BurCtx c{r - slot * GS, lane, m.dim / CPL};
   if (chain >= s.n_chains) return;
   T* row = lds + (threadIdx.x & ~(GS - 1)) * CPL;
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
   T* u = (T*)s.u + chain * 3;
-  T ur[3] = {u[0], u[1], u[2]};  // every lane of the group keeps the chain state
+  T ur[3] = {u[0], u[1], u[2]};  // every lane of the chain keeps the chain state
   const T* sq = (const T*)s.prior_sqrt;
   const T beta = (T)s.beta, contr = (T)s.contraction;
   T* phi = (T*)s.phi;
   T phu = phi[chain];
-  int64_t nacc = 0, ncalls = 0;
-  for (int64_t st = 0; st < s.n_steps; ++st) {
-    const uint64_t step = s.step0 + (uint64_t)st;
-    const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
-    const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
-    T v[3];
-    pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, s.proposal == IPMC_PROPOSAL_RW);
-    bool ok = true;
-    if (s.box_lo || s.box_hi) {
-      const T* lo = (const T*)s.box_lo;
-      const T* hi = (const T*)s.box_hi;
-      const T* off = (const T*)s.box_off;
+  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
+  int nacc = 0, ncalls = 0;
+  int64_t st = 0;
+  while (st < s.n_steps) {
+    const int64_t left = s.n_steps - st;
+    const int64_t tt = st + slot;
+    bool ok = false, acc = false;
+    T phv = (T)0;
+    T v[3] = {(T)0, (T)0, (T)0};
+    if (slot < left) {  // uniform per slot
+      const uint64_t step = s.step0 + (uint64_t)tt;
+      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
+      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
+      pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, s.proposal == IPMC_PROPOSAL_RW);
+      ok = true;
+      if (s.box_lo || s.box_hi) {
+        const T* lo = (const T*)s.box_lo;
+        const T* hi = (const T*)s.box_hi;
+        const T* off = (const T*)s.box_off;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const T t = v[j] + (off ? off[j] : (T)0);
-        if (lo && !(lo[j] < t)) ok = false;
-        if (hi && !(t < hi[j])) ok = false;
+        for (int j = 0; j < 3; ++j) {
+          const T t = v[j] + (off ? off[j] : (T)0);
+          if (lo && !(lo[j] < t)) ok = false;
+          if (hi && !(t < hi[j])) ok = false;
+        }
+      }
+      if (ok) {
+        phv = burgers_phi<T, CPL, GS, FM>(m, v, c, row, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
+        phv = __shfl(phv, lane & ~(GS - 1), 64);
+        if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
+        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
       }
     }
-    if (ok) {
-      ++ncalls;
-      T phv = burgers_phi<T, CPL, GS, FM>(m, v, c, row, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
-      phv = __shfl(phv, lane & ~(GS - 1), 64);
-      if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
-      if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
+    // one bit per slot (its first lane, bit slot*GS of the chain's lanes)
+    const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
+    const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
+    const int first = accm ? __builtin_ctzll(accm) / GS : S;
+    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
+    const int ubits = used * GS;
+    ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+    const int wl = cbase + (first < S ? first : 0) * GS;
+    T vf[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) ur[j] = v[j];
-        phu = phv;
-        ++nacc;
+    for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
+    const T phf = __shfl(phv, wl, 64);
+    if (s.sum_u && r == 0) {
+      for (int q = 0; q < used; ++q) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double ud = (q == first) ? (double)vf[j] : (double)ur[j];
+          s.sum_u[chain * 3 + j] += ud;
+          if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+        }
       }
     }
-    if (s.sum_u && c.sub == 0) {
+    if (first < S) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double ud = (double)ur[j];
-        s.sum_u[chain * 3 + j] += ud;
-        if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
-      }
+      for (int j = 0; j < 3; ++j) ur[j] = vf[j];
+      phu = phf;
+      ++nacc;
     }
+    st += used;
   }
-  if (c.sub == 0) {
+  if (r == 0) {
     phi[chain] = phu;
     if (s.accepts) s.accepts[chain] += nacc;
     if (s.calls) s.calls[chain] += ncalls;
@@ -362,10 +393,30 @@ static bool pick(int N, int64_t n_chains, int lanes, int& cpl, int& gs) {
   return fit(N, 8, cpl, gs) || fit(N, 4, cpl, gs);
 }
 
+// Speculation width: spec_width if given (a power of two, S·GS <= 64), else for
+// multi-step launches the widest keeping the ensemble within one wave per SIMD.
+template <int GS>
+static int burgers_spec(const ipmc_sweep& s) {
+  if (s.spec_width > 0) {
+    const int w = s.spec_width;
+    return ((w & (w - 1)) == 0 && w * GS <= 64) ? w : -1;
+  }
+  int w = 1;
+  if (s.n_steps > 1)
+    while (w * 2 * GS <= 64 && s.n_chains * (int64_t)GS * w * 2 <= 65536) w *= 2;
+  return w;
+}
+
 template <typename T, int CPL, int GS, bool FM>
 static int launch_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
-  const int64_t blocks = (s.n_chains * GS + kBurBlock - 1) / kBurBlock;
-  hipLaunchKernelGGL((burgers_sweep_kernel<T, CPL, GS, FM>), dim3((unsigned)blocks), dim3(kBurBlock), 0, st, m, s);
+  const int S = burgers_spec<GS>(s);
+  if (S < 1) {
+    set_error("Burgers: spec_width must be a power of two with spec_width * %d lanes <= 64", GS);
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  const int64_t blocks = (s.n_chains * GS * S + kBurBlock - 1) / kBurBlock;
+  hipLaunchKernelGGL((burgers_sweep_kernel<T, CPL, GS, FM>), dim3((unsigned)blocks), dim3(kBurBlock), 0, st, m, s,
+                     S);
   return check_launch("burgers_sweep_kernel");
 }
 

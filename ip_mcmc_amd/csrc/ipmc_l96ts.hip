@@ -186,11 +186,22 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
   return (T)0.5 * s;
 }
 
+// Sweep with S speculative slots per chain (S = 1: the plain sequential chain).
+// A chain owns S consecutive K-lane groups; slot s evaluates step st+s from the
+// current state as if the steps before it in the round were rejected, and the
+// first accepting slot ends the round (see small_spec_kernel) -- bit-identical
+// to S = 1.  ⌊64 / (S·K)⌋ chains per wave.
 template <typename T, int J, bool FM>
-__global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
+__global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kernel(const ipmc_model m, const ipmc_sweep s,
+                                                                                 int S) {
   const int lane = threadIdx.x & 63;
-  TsCtx c;
-  const int64_t chain = ts_chain(m.dim, c);
+  const int K = m.dim, G = S * K;
+  const int cpw = 64 / G;
+  const int q = lane / G, r = lane - q * G;
+  const int slot = r / K;
+  const int cbase = q * G;  // the chain's first lane in the wave
+  TsCtx c{K, r - slot * K, cbase + slot * K};
+  const int64_t chain = q < cpw ? (((int64_t)blockIdx.x * kTsBlock + threadIdx.x) >> 6) * cpw + q : -1;
   if (chain < 0 || chain >= s.n_chains) return;
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
   T* u = (T*)s.u + chain * 3;
@@ -200,48 +211,71 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kern
   const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
   T* phi = (T*)s.phi;
   T phu = phi[chain];
-  int64_t nacc = 0, ncalls = 0;
-  for (int64_t st = 0; st < s.n_steps; ++st) {
-    const uint64_t step = s.step0 + (uint64_t)st;
-    const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
-    const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
+  int nacc = 0, ncalls = 0;
+  int64_t st = 0;
+  while (st < s.n_steps) {
+    const int64_t left = s.n_steps - st;
+    const int64_t tt = st + slot;
     int kq = c.sub;
     asm volatile("" : "+v"(kq));
-    T v[3];
-    pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw);
-    bool ok = true;
-    if (s.box_lo || s.box_hi) {
-      const T* lo = (const T*)s.box_lo;
-      const T* hi = (const T*)s.box_hi;
-      const T* off = (const T*)s.box_off;
+    bool ok = false, acc = false;
+    T phv = (T)0;
+    T v[3] = {(T)0, (T)0, (T)0};
+    if (slot < left) {  // uniform per slot
+      const uint64_t step = s.step0 + (uint64_t)tt;
+      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
+      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
+      pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw);
+      ok = true;
+      if (s.box_lo || s.box_hi) {
+        const T* lo = (const T*)s.box_lo;
+        const T* hi = (const T*)s.box_hi;
+        const T* off = (const T*)s.box_off;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const T t = v[j] + (off ? off[j] : (T)0);
-        if (lo && !(lo[j] < t)) ok = false;
-        if (hi && !(t < hi[j])) ok = false;
+        for (int j = 0; j < 3; ++j) {
+          const T t = v[j] + (off ? off[j] : (T)0);
+          if (lo && !(lo[j] < t)) ok = false;
+          if (hi && !(t < hi[j])) ok = false;
+        }
+      }
+      if (ok) {
+        phv = ts_phi<T, J, FM>(m, v, c, kq, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
+        if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
+        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
       }
     }
-    if (ok) {
-      ++ncalls;
-      T phv = ts_phi<T, J, FM>(m, v, c, kq, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
-      if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
-      if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
+    // one bit per slot (its lane k = 0, at bit slot*K of the chain's lanes)
+    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
+    const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
+    const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
+    const int first = accm ? __builtin_ctzll(accm) / K : S;
+    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
+    const int ubits = used * K;
+    ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+    const int wl = cbase + (first < S ? first : 0) * K;  // the winning slot's lane k = 0
+    T vf[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) ur[j] = v[j];
-        phu = phv;
-        ++nacc;
+    for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
+    const T phf = __shfl(phv, wl, 64);
+    if (s.sum_u && r == 0) {
+      for (int qq = 0; qq < used; ++qq) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const double ud = (qq == first) ? (double)vf[j] : (double)ur[j];
+          s.sum_u[chain * 3 + j] += ud;
+          if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+        }
       }
     }
-    if (s.sum_u && c.sub == 0) {
+    if (first < S) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double ud = (double)ur[j];
-        s.sum_u[chain * 3 + j] += ud;
-        if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
-      }
+      for (int j = 0; j < 3; ++j) ur[j] = vf[j];
+      phu = phf;
+      ++nacc;
     }
+    st += used;
   }
-  if (c.sub == 0) {
+  if (r == 0) {
     phi[chain] = phu;
     if (s.accepts) s.accepts[chain] += nacc;
     if (s.calls) s.calls[chain] += ncalls;
@@ -275,13 +309,28 @@ static int64_t ts_blocks(int K, int64_t n) {
 
 #define IPMC_TS_J(X) X(1) X(2) X(4) X(8) X(10) X(16)
 
+// Speculation width: spec_width if given (S·K <= 64), else, for multi-step
+// launches, the widest that keeps the ensemble within one wave per SIMD.
+static int ts_spec(const ipmc_model& m, const ipmc_sweep& s) {
+  const int K = m.dim, smax = 64 / K;
+  if (s.spec_width > 0) return s.spec_width <= smax ? s.spec_width : -1;
+  if (s.n_steps <= 1) return 1;
+  const int64_t fit = 65536 / (s.n_chains * (int64_t)K);
+  return (int)(fit < 1 ? 1 : (fit > smax ? smax : fit));
+}
+
 template <typename T, bool FM>
 static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
-  const int64_t blocks = ts_blocks(m.dim, s.n_chains);
+  const int S = ts_spec(m, s);
+  if (S < 1) {
+    set_error("two-scale Lorenz-96: spec_width * K must be <= 64");
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  const int64_t blocks = ts_blocks(m.dim * S, s.n_chains);
   switch (m.fast_per_slow) {
-#define IPMC_J(J)                                                                                             \
-  case J:                                                                                                     \
-    hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s);     \
+#define IPMC_J(J)                                                                                              \
+  case J:                                                                                                      \
+    hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, S);  \
     return check_launch("l96ts_sweep_kernel");
     IPMC_TS_J(IPMC_J)
 #undef IPMC_J

@@ -47,7 +47,8 @@ def _model(rng, case):
 
 
 def _layout(rng, op, info, dtype):
-    from ip_mcmc_amd import BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator
+    from ip_mcmc_amd import (BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator,
+                             TwoScaleLorenz96Operator)
 
     if isinstance(op, Lorenz96Operator):
         d = info["d"]
@@ -59,9 +60,14 @@ def _layout(rng, op, info, dtype):
     if isinstance(op, BurgersOperator):
         N = info["N"]
         opts = [lp for lp in (16, 32, 64) if N % lp == 0 and N // lp in (4, 8)]
-        return (int(rng.choice(opts)) if opts and rng.random() < 0.5 else 0), 0, 1
+        lanes = int(rng.choice(opts)) if opts and rng.random() < 0.5 else 0
+        need = lanes if lanes else N // (8 if N % 8 == 0 else 4)
+        gs = min(g for g in (16, 32, 64) if g >= need)
+        return lanes, 0, int(rng.choice([w for w in (0, 1, 2, 4) if w * gs <= 64]))
     if isinstance(op, (LinearOperator, Lorenz63Operator)) and op.k <= 8:
         return 0, 0, int(rng.choice([0, 1, 2, 4, 16, 64]))
+    if isinstance(op, TwoScaleLorenz96Operator):
+        return 0, 0, int(rng.integers(0, 64 // op.K + 1))
     return 0, 0, 1
 
 

@@ -672,3 +672,40 @@ def test_l96_speculative_sweeps_bit_exact(dev, orc, dtype):
         d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, lanes=lanes_list[-1], cpl=1,
                           spec=4, proposal="rw", reg_scale=rs)
         _assert_same(d, o, (K, "rw"))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
+    """Speculative slots in the two-scale (S·K lanes per chain) and Burgers
+    (S·GS lanes) sweeps equal the sequential chain bit for bit."""
+    from ip_mcmc_amd import BurgersOperator, TwoScaleLorenz96Operator
+
+    n = 17
+    sched = np.stack([np.linspace(0.05, 0.3, n), np.sqrt(1 - np.linspace(0.05, 0.3, n) ** 2)], axis=1)
+    rng = np.random.default_rng(31)
+    cases = []
+    for K, J, arith in ((6, 4, "fma"), (3, 1, "reference"), (11, 2, "fma")):
+        op = TwoScaleLorenz96Operator(K=K, J=J, x0=rng.normal(size=K * (1 + J)), dt=0.004, n_steps=25, arith=arith)
+        cases.append((op, (0, 2, 64 // K)))
+    for N, arith in ((128, "reference"), (256, "fma")):
+        op = BurgersOperator(N=N, dt_mode="cfl", T=0.2, arith=arith)
+        cases.append((op, (0, 2, 4) if N == 128 else (0, 2)))
+    for op, widths in cases:
+        U0, phi0, y, ginv, sq = _problem(op, 19, dtype, orc, seed=3)
+        ginv = ginv * 0.2  # broad enough for acceptances inside the rounds
+        phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
+        for kw in (dict(), dict(box=(np.full(3, -0.3), None, None), sched=sched), dict(want_sums=True)):
+            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 8, 2**32 - 3, n, dtype, **kw)
+            assert 0 < o["acc"].sum() < 19 * n, (type(op).__name__, o["acc"].sum())
+            for w in widths:
+                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 8, 2**32 - 3, n, dtype, dev, spec=w, **kw)
+                _assert_same(d, o, (type(op).__name__, op.arith, w, list(kw)))
+                assert np.array_equal(d["samp"], o["u"])
+                if "want_sums" in kw:
+                    assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
+        rs = np.array([0.5, 1.0, 2.0])
+        phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
+        o = _sweep_oracle(orc, op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, proposal="rw", reg_scale=rs)
+        d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, spec=widths[-1], proposal="rw",
+                          reg_scale=rs)
+        _assert_same(d, o, (type(op).__name__, "rw"))
