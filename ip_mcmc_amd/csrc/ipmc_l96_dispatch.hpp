@@ -10,7 +10,8 @@ namespace ipmc {
 // State dims with a compiled kernel. Each (D, LPC) needs M = D/LPC >= 2
 // components per lane and at most 160 B of state per lane-array (6 arrays of
 // M live in VGPRs).
-#define IPMC_L96_DIMS(X) X(4) X(8) X(16) X(20) X(32) X(36) X(40) X(64) X(128) X(256)
+#define IPMC_L96_DIMS(X) \
+  X(4) X(6) X(8) X(10) X(12) X(16) X(20) X(24) X(32) X(36) X(40) X(48) X(60) X(64) X(80) X(128) X(160) X(256)
 
 template <typename T, int D, int LPC>
 constexpr bool l96_ok() {

@@ -16,8 +16,9 @@ pytestmark = pytest.mark.gpu
 
 from test_gpu_parity import _assert_same, _np, _sweep_device, _sweep_oracle  # noqa: E402
 
-L96_DIMS = {4: (1, 2), 8: (1, 2, 4), 16: (1, 2, 4, 8), 20: (1, 2, 4), 32: (2, 4, 8, 16), 36: (2, 4),
-            40: (2, 4, 8), 64: (4, 8, 16), 128: (8, 16)}
+L96_DIMS = {4: (1, 2), 6: (1, 2), 8: (1, 2, 4), 10: (1, 2), 12: (1, 2, 4), 16: (1, 2, 4, 8), 20: (1, 2, 4),
+            24: (2, 4, 8), 32: (2, 4, 8, 16), 36: (2, 4), 40: (2, 4, 8), 48: (4, 8, 16), 60: (4,),
+            64: (4, 8, 16), 80: (4, 8, 16), 128: (8, 16), 160: (8, 16)}
 
 
 def _model(rng, case):

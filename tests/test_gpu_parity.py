@@ -184,7 +184,8 @@ def test_sweep_small_models_bit_exact(dev, orc, dtype):
 
 
 @pytest.mark.parametrize("dtype,cpl", [(torch.float64, 1), (torch.float32, 1), (torch.float32, 2)])
-@pytest.mark.parametrize("K,lanes", [(8, 1), (8, 2), (8, 4), (40, 1), (40, 2), (40, 4), (40, 8), (32, 16), (64, 16)])
+@pytest.mark.parametrize("K,lanes", [(8, 1), (8, 2), (8, 4), (40, 1), (40, 2), (40, 4), (40, 8), (32, 16), (64, 16),
+                                     (6, 2), (10, 2), (60, 4), (80, 16)])
 def test_sweep_l96_bit_exact_every_layout(dev, orc, dtype, cpl, K, lanes):
     """Every (lanes per chain, chains per lane) layout gives the oracle's bits;
     131 chains so the packed fp32 layout has a phantom partner in its last pair."""

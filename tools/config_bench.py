@@ -6,6 +6,7 @@ cfg2     Lorenz-63, 500 RK4 steps, 4 096 chains
 cfg4     Burgers N=256, fixed dt 1e-3 x 1000, 2 048 chains (= 16 384 / 8 GPUs)
 cfg4full Burgers as cfg4 with all 16 384 chains on one GPU
 cfg4cfl  Burgers N=256, reference CFL time stepping, 2 048 chains
+cfg4visc Burgers N=256 with viscosity nu = 1e-3 (central differences), fixed dt 1e-3 x 1000, 2 048 chains
 cfg5     Lorenz-96 d=256, 10 000 RK4 steps, 131 072 chains (= 2^20 / 8 GPUs)
 l96xN    the headline problem with N = 1, 64 or 1024 chains (speculative sweeps)
 ts6      two-scale Lorenz-96 K=6 J=4 (the thesis problem, lorenz_mcmc.py:87-88), T=20 (4 000 RK4 steps), 65 536 chains
@@ -31,9 +32,11 @@ def make(cfg):
         x0 = Lorenz63Operator.spinup(n_steps=1000)
         op = Lorenz63Operator(x0=x0, dt=0.01, n_steps=500)
         return op, 4096, 0.2, np.array([1.0, 1.0, np.sqrt(0.1)]), 80 * 500, 1.0
-    if cfg in ("cfg4", "cfg4full", "cfg4cfl"):
+    if cfg in ("cfg4", "cfg4full", "cfg4cfl", "cfg4visc"):
         if cfg == "cfg4cfl":
             op = BurgersOperator(N=256, dt_mode="cfl")
+        elif cfg == "cfg4visc":  # BASELINE's "viscous Burgers": central-difference diffusion, nu = 1e-3
+            op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000, nu=1e-3)
         else:
             op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000)
         n = 16384 if cfg == "cfg4full" else 2048
