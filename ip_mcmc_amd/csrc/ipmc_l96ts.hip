@@ -19,9 +19,10 @@ constexpr int kTsBlock = 256;
 
 // Occupancy target (waves per SIMD) for the sweep kernel: 4 RK4 arrays of
 // 1 + J values per lane plus the chain state.
-template <typename T, int J>
+template <typename T, int J, int SPL>
 constexpr int ts_waves() {
-  return sizeof(T) == 8 ? (J <= 4 ? 4 : (J <= 10 ? 3 : 2)) : (J <= 2 ? 5 : (J <= 10 ? 4 : 3));
+  if constexpr (SPL == 2) return sizeof(T) == 8 ? (J <= 4 ? 3 : 2) : (J <= 2 ? 4 : (J <= 8 ? 3 : 2));
+  return sizeof(T) == 8 ? (J <= 4 ? 4 : (J <= 10 ? 3 : 2)) : (J <= 2 ? 5 : (J <= 8 ? 4 : (J <= 10 ? 3 : 2)));
 }
 
 struct TsCtx {
@@ -74,39 +75,95 @@ __device__ __forceinline__ T block_mean(const T (&s)[1 + J]) {
   return np_pairwise<T, J>(y, 0) / (T)J;
 }
 
-template <typename T, int J, bool FM>
-__device__ __forceinline__ void ts_rhs(const T (&s)[1 + J], T F, T hc, T hJ, T bb, T cc, const TsCtx& c,
-                                       T (&o)[1 + J]) {
-  const int K = c.K;
-  const T X = s[0];
-  const T xm1 = __shfl(X, c.base + (c.sub + K - 1) % K, 64);
-  const T xm2 = __shfl(X, c.base + (c.sub + K - 2) % K, 64);
-  const T xp1 = __shfl(X, c.base + (c.sub + 1) % K, 64);
-  const T yb = block_mean<T, J>(s);
+// dX_k/dt (lorenz.py:77-86) and dY_{k,j}/dt (lorenz.py:94-99).
+template <typename T, bool FM>
+__device__ __forceinline__ T ts_slow(T X, T xm1, T xm2, T xp1, T F, T hc, T yb) {
   if constexpr (FM) {
     const T t = madd<true>(xp1 - xm2, xm1, F - X);
-    o[0] = madd<true>(-hc, yb, t);
+    return madd<true>(-hc, yb, t);
   } else {
     T t = -X;
     t = t - (xm1 * xm2 - xm1 * xp1);
     t = t + F;
-    o[0] = t - hc * yb;
+    return t - hc * yb;
+  }
+}
+
+template <typename T, bool FM>
+__device__ __forceinline__ T ts_fast(T y, T yp1, T yp2, T ym1, T X, T hJ, T bb, T cc) {
+  T t;
+  if constexpr (FM) {
+    const T nl = yp1 * (yp2 - ym1);
+    t = madd<true>(hJ, X, -y);
+    t = madd<true>(-bb, nl, t);
+  } else {
+    t = -y;
+    t = t - bb * (yp1 * yp2 - ym1 * yp1);
+    t = t + hJ * X;
+  }
+  return t * cc;
+}
+
+// One classical RK4 stage over the lane's SPL slow variables k = sub*SPL + a
+// and their fast blocks, with each rate k consumed as soon as it is computed:
+//   STAGE 1: acc = k;           out = base + c*k     (in = x, out = xs)
+//   STAGE 2/3: acc = 2k + acc;  out = base + c*k     (in = out = xs)
+//   STAGE 4: acc = acc + k;     out = base + c*acc   (in = xs, out = x)
+// -- the same operations as the textbook form, so the bits do not change, but
+// no separate array of rates: `in` may alias `out` because every value an
+// element still needs is read before it is overwritten (the old X and block
+// mean, the old Y_{k,0}, Y_{k,1} for the cyclic wrap and the previous old Y).
+// Slow neighbours across lanes come by ds_bpermute, cyclic over the group's
+// L = K/SPL lanes, before anything is written.
+template <typename T, int J, bool FM, int SPL, int STAGE>
+__device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + J], T (&base)[SPL][1 + J],
+                                         T (&acc)[SPL][1 + J], T cst, T F, T hc, T hJ, T bb, T cc, const TsCtx& c) {
+  auto upd = [&](int a, int i, T k) {
+    if constexpr (STAGE == 1) acc[a][i] = k;
+    else if constexpr (STAGE == 4) acc[a][i] = acc[a][i] + k;
+    else acc[a][i] = madd<FM>((T)2, k, acc[a][i]);
+    if constexpr (STAGE == 4) out[a][i] = madd<FM>(cst, acc[a][i], base[a][i]);
+    else out[a][i] = madd<FM>(cst, k, base[a][i]);
+  };
+  const int L = c.K / SPL;
+  T Xo[SPL], yb[SPL], kX[SPL];
+#pragma unroll
+  for (int a = 0; a < SPL; ++a) {
+    Xo[a] = in[a][0];
+    yb[a] = block_mean<T, J>(in[a]);
+  }
+  if constexpr (SPL == 1) {
+    const T xm1 = __shfl(Xo[0], c.base + (c.sub + L - 1) % L, 64);
+    const T xm2 = __shfl(Xo[0], c.base + (c.sub + L - 2) % L, 64);
+    const T xp1 = __shfl(Xo[0], c.base + (c.sub + 1) % L, 64);
+    kX[0] = ts_slow<T, FM>(Xo[0], xm1, xm2, xp1, F, hc, yb[0]);
+  } else {
+    const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
+    const T p1 = __shfl(Xo[SPL - 1], prev, 64);  // X_{k0-1}
+    const T p2 = __shfl(Xo[SPL - 2], prev, 64);  // X_{k0-2}
+    const T n0 = __shfl(Xo[0], next, 64);        // X_{k0+SPL}
+#pragma unroll
+    for (int a = 0; a < SPL; ++a) {
+      const T xm1 = a >= 1 ? Xo[a - 1] : p1;
+      const T xm2 = a >= 2 ? Xo[a - 2] : (a == 1 ? p1 : p2);
+      const T xp1 = a + 1 < SPL ? Xo[a + 1] : n0;
+      kX[a] = ts_slow<T, FM>(Xo[a], xm1, xm2, xp1, F, hc, yb[a]);
+    }
   }
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    const T y = s[1 + j];
-    const T yp1 = s[1 + (j + 1) % J], yp2 = s[1 + (j + 2) % J], ym1 = s[1 + (j + J - 1) % J];
-    T t;
-    if constexpr (FM) {
-      const T nl = yp1 * (yp2 - ym1);
-      t = madd<true>(hJ, X, -y);
-      t = madd<true>(-bb, nl, t);
-    } else {
-      t = -y;
-      t = t - bb * (yp1 * yp2 - ym1 * yp1);
-      t = t + hJ * X;
+  for (int a = 0; a < SPL; ++a) {
+    upd(a, 0, kX[a]);
+    const T y0 = in[a][1], y1 = in[a][1 + (1 % J)];
+    T prev = in[a][J];  // old Y_{k,J-1}: the j = 0 element's left neighbour
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const T y = in[a][1 + j];  // elements >= j are not yet overwritten
+      const T yp1 = (j + 1 < J) ? in[a][2 + j] : y0;
+      const T yp2 = (j + 2 < J) ? in[a][3 + j] : ((j + 2 - J) == 0 ? y0 : y1);
+      const T k = ts_fast<T, FM>(y, yp1, yp2, prev, Xo[a], hJ, bb, cc);
+      prev = y;
+      upd(a, 1 + j, k);
     }
-    o[1 + j] = t * cc;
   }
 }
 
@@ -114,71 +171,64 @@ __device__ __forceinline__ void ts_rhs(const T (&s)[1 + J], T F, T hc, T hJ, T b
 // kq: k behind an opaque register copy made once per pCN step, so the
 // per-lane constants (x0 block, y, 1/gamma) are re-read each step instead of
 // being hoisted into VGPRs for the whole sweep.
-template <typename T, int J, bool FM>
+template <typename T, int J, bool FM, int SPL>
 __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq, const T* __restrict__ y,
                     const T* __restrict__ ginv, T* g_out) {
   const int K = c.K;
-  const int k = kq;
+  const int k0 = kq * SPL;  // this lane's first slow variable
   const T* th0 = (const T*)m.theta0;
   const T F = th0[0] + v[0], h = th0[1] + v[1], bb = th0[2] + v[2];
   const T cc = (T)m.coupling_c;
   const T hc = h * cc, hJ = h / (T)J;
   const T hh = (T)m.dt, h2 = hh * (T)0.5, h6 = hh / (T)6;
   const T* x0 = (const T*)m.x0;
-  T x[1 + J];
-  x[0] = x0[k];
+  T x[SPL][1 + J];
+  T ob[SPL][5];
 #pragma unroll
-  for (int j = 0; j < J; ++j) x[1 + j] = x0[K + k * J + j];
-  T ob[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < SPL; ++i) {
+    x[i][0] = x0[k0 + i];
+#pragma unroll
+    for (int j = 0; j < J; ++j) x[i][1 + j] = x0[K + (k0 + i) * J + j];
+#pragma unroll
+    for (int b = 0; b < 5; ++b) ob[i][b] = (T)0;
+  }
   const bool refmom = (m.moment_mode == 0);
   for (int n = 0; n < m.n_steps; ++n) {
-    T k1[1 + J], acc[1 + J], xs[1 + J];
-    ts_rhs<T, J, FM>(x, F, hc, hJ, bb, cc, c, k1);
+    T acc[SPL][1 + J], xs[SPL][1 + J];
+    ts_stage<T, J, FM, SPL, 1>(x, xs, x, acc, h2, F, hc, hJ, bb, cc, c);
+    ts_stage<T, J, FM, SPL, 2>(xs, xs, x, acc, h2, F, hc, hJ, bb, cc, c);
+    ts_stage<T, J, FM, SPL, 3>(xs, xs, x, acc, hh, F, hc, hJ, bb, cc, c);
+    ts_stage<T, J, FM, SPL, 4>(xs, x, x, acc, h6, F, hc, hJ, bb, cc, c);
 #pragma unroll
-    for (int i = 0; i <= J; ++i) {
-      acc[i] = k1[i];
-      xs[i] = madd<FM>(h2, k1[i], x[i]);
+    for (int a = 0; a < SPL; ++a) {
+      const T X = x[a][0];
+      const T yb = refmom ? x[a][1] : block_mean<T, J>(x[a]);
+      ob[a][0] = ob[a][0] + X;
+      ob[a][1] = ob[a][1] + yb;
+      ob[a][2] = madd<FM>(X, X, ob[a][2]);
+      ob[a][3] = madd<FM>(X, yb, ob[a][3]);
+      ob[a][4] = madd<FM>(yb, yb, ob[a][4]);
     }
-    ts_rhs<T, J, FM>(xs, F, hc, hJ, bb, cc, c, k1);
-#pragma unroll
-    for (int i = 0; i <= J; ++i) {
-      acc[i] = madd<FM>((T)2, k1[i], acc[i]);
-      xs[i] = madd<FM>(h2, k1[i], x[i]);
-    }
-    ts_rhs<T, J, FM>(xs, F, hc, hJ, bb, cc, c, k1);
-#pragma unroll
-    for (int i = 0; i <= J; ++i) {
-      acc[i] = madd<FM>((T)2, k1[i], acc[i]);
-      xs[i] = madd<FM>(hh, k1[i], x[i]);
-    }
-    ts_rhs<T, J, FM>(xs, F, hc, hJ, bb, cc, c, k1);
-#pragma unroll
-    for (int i = 0; i <= J; ++i) {
-      acc[i] = acc[i] + k1[i];
-      x[i] = madd<FM>(h6, acc[i], x[i]);
-    }
-    const T X = x[0];
-    const T yb = refmom ? x[1] : block_mean<T, J>(x);
-    ob[0] = ob[0] + X;
-    ob[1] = ob[1] + yb;
-    ob[2] = madd<FM>(X, X, ob[2]);
-    ob[3] = madd<FM>(X, yb, ob[3]);
-    ob[4] = madd<FM>(yb, yb, ob[4]);
   }
   const T nn = (T)m.n_steps;
-  T r[5];
+  T r[SPL][5];
 #pragma unroll
-  for (int b = 0; b < 5; ++b) {
-    const T g = ob[b] / nn;
-    if (g_out) g_out[b * K + k] = g;
-    r[b] = y ? (y[b * K + k] - g) * ginv[b * K + k] : (T)0;
-  }
+  for (int a = 0; a < SPL; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const int k = k0 + a;
+      const T g = ob[a][b] / nn;
+      if (g_out) g_out[b * K + k] = g;
+      r[a][b] = y ? (y[b * K + k] - g) * ginv[b * K + k] : (T)0;
+    }
   T s = (T)0;
   if (y) {
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
-      for (int kk = 0; kk < K; ++kk) {
-        const T val = __shfl(r[b], c.base + kk, 64);
+      for (int kk = 0; kk < K; ++kk) {  // observation order: slow variable kk of moment b
+        T mine = r[0][b];
+        if constexpr (SPL == 2) mine = (kk & 1) ? r[1][b] : r[0][b];
+        const T val = __shfl(mine, c.base + kk / SPL, 64);
         s = madd<FM>(val, val, s);
       }
     }
@@ -187,20 +237,20 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
 }
 
 // Sweep with S speculative slots per chain (S = 1: the plain sequential chain).
-// A chain owns S consecutive K-lane groups; slot s evaluates step st+s from the
-// current state as if the steps before it in the round were rejected, and the
-// first accepting slot ends the round (see small_spec_kernel) -- bit-identical
-// to S = 1.  ⌊64 / (S·K)⌋ chains per wave.
-template <typename T, int J, bool FM>
-__global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kernel(const ipmc_model m, const ipmc_sweep s,
-                                                                                 int S) {
+// A chain owns S consecutive groups of L = K/SPL lanes; slot s evaluates step
+// st+s from the current state as if the steps before it in the round were
+// rejected, and the first accepting slot ends the round (see
+// small_spec_kernel) -- bit-identical to S = 1.  ⌊64 / (S·L)⌋ chains per wave.
+template <typename T, int J, bool FM, int SPL>
+__global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep_kernel(const ipmc_model m,
+                                                                                      const ipmc_sweep s, int S) {
   const int lane = threadIdx.x & 63;
-  const int K = m.dim, G = S * K;
+  const int K = m.dim, L = K / SPL, G = S * L;
   const int cpw = 64 / G;
   const int q = lane / G, r = lane - q * G;
-  const int slot = r / K;
+  const int slot = r / L;
   const int cbase = q * G;  // the chain's first lane in the wave
-  TsCtx c{K, r - slot * K, cbase + slot * K};
+  TsCtx c{K, r - slot * L, cbase + slot * L};
   const int64_t chain = q < cpw ? (((int64_t)blockIdx.x * kTsBlock + threadIdx.x) >> 6) * cpw + q : -1;
   if (chain < 0 || chain >= s.n_chains) return;
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
@@ -239,20 +289,20 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kern
         }
       }
       if (ok) {
-        phv = ts_phi<T, J, FM>(m, v, c, kq, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
+        phv = ts_phi<T, J, FM, SPL>(m, v, c, kq, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
         if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
         acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
       }
     }
-    // one bit per slot (its lane k = 0, at bit slot*K of the chain's lanes)
+    // one bit per slot (its first lane, at bit slot*L of the chain's lanes)
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
     const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
     const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-    const int first = accm ? __builtin_ctzll(accm) / K : S;
+    const int first = accm ? __builtin_ctzll(accm) / L : S;
     const int used = first < S ? first + 1 : (int)(left < S ? left : S);
-    const int ubits = used * K;
+    const int ubits = used * L;
     ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-    const int wl = cbase + (first < S ? first : 0) * K;  // the winning slot's lane k = 0
+    const int wl = cbase + (first < S ? first : 0) * L;  // the winning slot's first lane
     T vf[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
@@ -289,49 +339,71 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J>())) void l96ts_sweep_kern
   }
 }
 
-template <typename T, int J, bool FM, bool PHI>
+template <typename T, int J, bool FM, int SPL, bool PHI>
 __global__ __launch_bounds__(kTsBlock) void l96ts_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
                                                               const T* __restrict__ y, const T* __restrict__ ginv,
                                                               T* __restrict__ out) {
   TsCtx c;
-  const int64_t chain = ts_chain(m.dim, c);
+  int64_t chain = ts_chain(m.dim / SPL, c);
+  c.K = m.dim;
   if (chain < 0 || chain >= n) return;
   const T v[3] = {uin[chain * 3], uin[chain * 3 + 1], uin[chain * 3 + 2]};
-  const T ph = ts_phi<T, J, FM>(m, v, c, c.sub, PHI ? y : nullptr, ginv, PHI ? nullptr : out + chain * m.q);
+  const T ph = ts_phi<T, J, FM, SPL>(m, v, c, c.sub, PHI ? y : nullptr, ginv, PHI ? nullptr : out + chain * m.q);
   if (PHI && c.sub == 0) out[chain] = ph;
 }
 
-static int64_t ts_blocks(int K, int64_t n) {
-  const int64_t cpw = 64 / K;
+// blocks for n chains of G lanes each, ⌊64/G⌋ chains per wave
+static int64_t ts_blocks(int G, int64_t n) {
+  const int64_t cpw = 64 / G;
   const int64_t waves = (n + cpw - 1) / cpw;
   return (waves * 64 + kTsBlock - 1) / kTsBlock;
 }
 
 #define IPMC_TS_J(X) X(1) X(2) X(4) X(8) X(10) X(16)
 
-// Speculation width: spec_width if given (S·K <= 64), else, for multi-step
+// Slow variables per lane: 2 when K is even, a chain would otherwise fill a
+// wave alone (K > 32: K=36 packs 3 chains = 54 lanes instead of 1 = 36) and the
+// doubled state still fits (J <= 10); 1 otherwise.  lanes_per_chain = K/2 or K
+// selects it explicitly.  -1: unsupported request.
+static int ts_spl(const ipmc_model& m, const ipmc_sweep* s) {
+  const int K = m.dim, J = m.fast_per_slow;
+  const bool two_ok = (K % 2 == 0) && J <= 10;
+  if (s && s->lanes_per_chain > 0) {
+    if (s->lanes_per_chain == K) return 1;
+    if (two_ok && s->lanes_per_chain == K / 2) return 2;
+    return -1;
+  }
+  return (two_ok && K > 32) ? 2 : 1;
+}
+
+// Speculation width: spec_width if given (S·L <= 64), else, for multi-step
 // launches, the widest that keeps the ensemble within one wave per SIMD.
-static int ts_spec(const ipmc_model& m, const ipmc_sweep& s) {
-  const int K = m.dim, smax = 64 / K;
+static int ts_spec(const ipmc_sweep& s, int L) {
+  const int smax = 64 / L;
   if (s.spec_width > 0) return s.spec_width <= smax ? s.spec_width : -1;
   if (s.n_steps <= 1) return 1;
-  const int64_t fit = 65536 / (s.n_chains * (int64_t)K);
+  const int64_t fit = 65536 / (s.n_chains * (int64_t)L);
   return (int)(fit < 1 ? 1 : (fit > smax ? smax : fit));
 }
 
-template <typename T, bool FM>
+template <typename T, bool FM, int SPL>
 static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
-  const int S = ts_spec(m, s);
+  const int L = m.dim / SPL;
+  const int S = ts_spec(s, L);
   if (S < 1) {
-    set_error("two-scale Lorenz-96: spec_width * K must be <= 64");
+    set_error("two-scale Lorenz-96: spec_width * lanes per chain (%d) must be <= 64", L);
     return IPMC_ERR_UNSUPPORTED;
   }
-  const int64_t blocks = ts_blocks(m.dim * S, s.n_chains);
+  const int64_t blocks = ts_blocks(L * S, s.n_chains);
   switch (m.fast_per_slow) {
-#define IPMC_J(J)                                                                                              \
-  case J:                                                                                                      \
-    hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, S);  \
-    return check_launch("l96ts_sweep_kernel");
+#define IPMC_J(J)                                                                                                  \
+  case J:                                                                                                          \
+    if constexpr (SPL == 1 || J <= 10) {                                                                           \
+      hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM, SPL>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, \
+                         S);                                                                                       \
+      return check_launch("l96ts_sweep_kernel");                                                                   \
+    }                                                                                                              \
+    break;
     IPMC_TS_J(IPMC_J)
 #undef IPMC_J
   }
@@ -339,20 +411,23 @@ static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) 
   return IPMC_ERR_UNSUPPORTED;
 }
 
-template <typename T, bool FM>
+template <typename T, bool FM, int SPL>
 static int ts_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
                      bool phi, hipStream_t st) {
-  const int64_t blocks = ts_blocks(m.dim, n);
+  const int64_t blocks = ts_blocks(m.dim / SPL, n);
   switch (m.fast_per_slow) {
-#define IPMC_J(J)                                                                                             \
-  case J:                                                                                                     \
-    if (phi)                                                                                                  \
-      hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, true>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, \
-                         n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                               \
-    else                                                                                                      \
-      hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, false>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st,   \
-                         m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                            \
-    return check_launch("l96ts_eval_kernel");
+#define IPMC_J(J)                                                                                                 \
+  case J:                                                                                                         \
+    if constexpr (SPL == 1 || J <= 10) {                                                                          \
+      if (phi)                                                                                                    \
+        hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, SPL, true>), dim3((unsigned)blocks), dim3(kTsBlock), 0,   \
+                           st, m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                          \
+      else                                                                                                        \
+        hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, SPL, false>), dim3((unsigned)blocks), dim3(kTsBlock), 0,  \
+                           st, m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                          \
+      return check_launch("l96ts_eval_kernel");                                                                   \
+    }                                                                                                             \
+    break;
     IPMC_TS_J(IPMC_J)
 #undef IPMC_J
   }
@@ -365,9 +440,18 @@ int l96ts_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
     set_error("two-scale Lorenz-96: K <= 64");
     return IPMC_ERR_UNSUPPORTED;
   }
+  const int spl = ts_spl(m, &s);
+  if (spl < 0) {
+    set_error("two-scale Lorenz-96: lanes_per_chain must be K or (K even, J <= 10) K/2");
+    return IPMC_ERR_UNSUPPORTED;
+  }
   const bool fm = m.arith == IPMC_ARITH_FMA;
-  if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true>(m, s, st) : ts_sweep_t<double, false>(m, s, st);
-  return fm ? ts_sweep_t<float, true>(m, s, st) : ts_sweep_t<float, false>(m, s, st);
+  if (spl == 2) {
+    if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true, 2>(m, s, st) : ts_sweep_t<double, false, 2>(m, s, st);
+    return fm ? ts_sweep_t<float, true, 2>(m, s, st) : ts_sweep_t<float, false, 2>(m, s, st);
+  }
+  if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true, 1>(m, s, st) : ts_sweep_t<double, false, 1>(m, s, st);
+  return fm ? ts_sweep_t<float, true, 1>(m, s, st) : ts_sweep_t<float, false, 1>(m, s, st);
 }
 
 int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
@@ -377,11 +461,18 @@ int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, con
     return IPMC_ERR_UNSUPPORTED;
   }
   const bool fm = m.arith == IPMC_ARITH_FMA;
+  if (ts_spl(m, nullptr) == 2) {
+    if (dtype == IPMC_F64)
+      return fm ? ts_eval_t<double, true, 2>(m, n, u, y, ginv, out, phi, st)
+                : ts_eval_t<double, false, 2>(m, n, u, y, ginv, out, phi, st);
+    return fm ? ts_eval_t<float, true, 2>(m, n, u, y, ginv, out, phi, st)
+              : ts_eval_t<float, false, 2>(m, n, u, y, ginv, out, phi, st);
+  }
   if (dtype == IPMC_F64)
-    return fm ? ts_eval_t<double, true>(m, n, u, y, ginv, out, phi, st)
-              : ts_eval_t<double, false>(m, n, u, y, ginv, out, phi, st);
-  return fm ? ts_eval_t<float, true>(m, n, u, y, ginv, out, phi, st)
-            : ts_eval_t<float, false>(m, n, u, y, ginv, out, phi, st);
+    return fm ? ts_eval_t<double, true, 1>(m, n, u, y, ginv, out, phi, st)
+              : ts_eval_t<double, false, 1>(m, n, u, y, ginv, out, phi, st);
+  return fm ? ts_eval_t<float, true, 1>(m, n, u, y, ginv, out, phi, st)
+            : ts_eval_t<float, false, 1>(m, n, u, y, ginv, out, phi, st);
 }
 
 }  // namespace ipmc
