@@ -72,9 +72,8 @@ struct RusConst {
   T mdx, c1, c2, nudx2;
 };
 
-template <typename T, int CPL, bool FM>
-__device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const RusConst<T>& k, bool visc,
-                                         T (&r)[CPL]) {
+template <typename T, int CPL, bool FM, bool VISC>
+__device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const RusConst<T>& k, T (&r)[CPL]) {
   T fl = FM ? rus_flux_fm<T>(hl, s[0], k.c1, k.c2) : rus_flux_ref<T>(hl, s[0]);
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
@@ -82,7 +81,7 @@ __device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const Ru
     const T left = (j > 0) ? s[j - 1] : hl;
     const T fr = FM ? rus_flux_fm<T>(s[j], right, k.c1, k.c2) : rus_flux_ref<T>(s[j], right);
     T v = FM ? fr - fl : (fr - fl) / k.mdx;
-    if (visc) {
+    if (VISC) {
       const T lap = (right - (s[j] + s[j])) + left;
       v = madd<FM>(k.nudx2, lap, v);
     }
@@ -111,8 +110,10 @@ __device__ __forceinline__ void halos(const T (&s)[CPL], T gl, T gr, const BurCt
 }
 
 // Integrate the Riemann IC (left, right, jump) to the end; returns validity.
-// w holds the final interior cells of this lane.
-template <typename T, int CPL, int GS, bool FM>
+// w holds the final interior cells of this lane.  VISC is a compile-time
+// switch: a runtime flag made the compiler evaluate the diffusion term for
+// every cell and select it away (6 extra VALU ops per cell and stage).
+template <typename T, int CPL, int GS, bool FM, bool VISC>
 __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, const BurCtx& c, T (&w)[CPL]) {
   const bool live = c.sub < c.nlive;
   const T* xc = (const T*)m.x0;
@@ -127,7 +128,6 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   T gr = (xc[N + 1] < jump) ? left : right;
   const T dx = (T)m.dx, mdx = -dx;
   const T cfl_dx = (T)m.cfl * dx;
-  const bool visc = (m.nu != 0.0);
   const T rdx = (T)1 / mdx;
   const RusConst<T> kc{mdx, (T)0.25 * rdx, (T)-0.5 * rdx, (T)m.nu / (dx * dx)};
   const T tend = (T)m.t_end;
@@ -158,12 +158,12 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
     // SSPRK2, rusanov.py:62-74
     T hl, hr, r[CPL], ws[CPL];
     halos<T, CPL>(w, gl, gr, c, hl, hr);
-    rus_rate<T, CPL, FM>(w, hl, hr, kc, visc, r);
+    rus_rate<T, CPL, FM, VISC>(w, hl, hr, kc, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) ws[j] = madd<FM>(dt, r[j], w[j]);
     const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
     halos<T, CPL>(ws, gls, grs, c, hl, hr);
-    rus_rate<T, CPL, FM>(ws, hl, hr, kc, visc, r);
+    rus_rate<T, CPL, FM, VISC>(ws, hl, hr, kc, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       ws[j] = madd<FM>(dt, r[j], ws[j]);
@@ -217,7 +217,8 @@ __device__ T burgers_phi(const ipmc_model& m, const T (&v)[3], const BurCtx& c, 
   const T right = th0[1] + v[1];
   const T jump = th0[2] + v[2];
   T w[CPL];
-  const bool valid = burgers_integrate<T, CPL, GS, FM>(m, left, right, jump, c, w);
+  const bool valid = (m.nu != 0.0) ? burgers_integrate<T, CPL, GS, FM, true>(m, left, right, jump, c, w)
+                                   : burgers_integrate<T, CPL, GS, FM, false>(m, left, right, jump, c, w);
   if (c.sub < c.nlive) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) row[c.sub * CPL + j] = w[j];

@@ -263,8 +263,24 @@ def test_headline_shape_subset_bit_exact(dev, orc):
     C_ = 65536
     rng = np.random.default_rng(21)
     idx = np.sort(rng.choice(C_, 48, replace=False))
+    from ip_mcmc_amd import _abi
+    from ip_mcmc_amd._lib import call
+
     for dtype in (torch.float32, torch.float64):
-        U0, phi0, y, ginv, sq = _problem(op, C_, dtype, orc, seed=21)
+        # Φ(u0) of the whole ensemble on the device (the oracle would need minutes
+        # for 65 536 chains x 2000 RK4 steps); the sampled chains' Φ is checked below
+        rng0 = np.random.default_rng(21)
+        U0 = (0.2 * rng0.normal(size=(C_, 40))).astype(_np(dtype)).astype(np.float64)
+        y = orc.forward(op, 0.1 * rng0.normal(size=(1, 40)))[0] + 0.05 * rng0.normal(size=40)
+        ginv = np.full(40, 1 / 0.05)
+        m, _ = op.model(dtype, dev)
+        Ut, yt, gt = _t(U0, dtype, dev), _t(y, dtype, dev), _t(ginv, dtype, dev)
+        pt = torch.empty(C_, dtype=dtype, device=dev)
+        call("ipmc_potential", C.byref(m), _abi.F64 if dtype == torch.float64 else _abi.F32, C_, Ut.data_ptr(),
+             yt.data_ptr(), gt.data_ptr(), pt.data_ptr(), _stream(dev))
+        phi0 = pt.cpu().numpy().astype(np.float64)
+        po = orc.potential(op, U0[idx], y, ginv, _np(dtype)).astype(np.float64)
+        assert np.array_equal(phi0[idx], po), dtype
         d = _sweep_device(op, U0, phi0, y, ginv, np.ones(40), 0.2, 5, 0, 1, dtype, dev)
         for i in idx:
             o = _sweep_oracle(orc, op, U0[i:i + 1], phi0[i:i + 1], y, ginv, np.ones(40), 0.2, 5, 0, 1, dtype,
