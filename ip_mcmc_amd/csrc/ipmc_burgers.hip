@@ -155,19 +155,30 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
       dt = dtf;
     }
     ++iters;
-    // SSPRK2, rusanov.py:62-74
+    // SSPRK2, rusanov.py:62-74.  REFERENCE: u* = u + dt L(u); u* += dt L(u*);
+    // u = (u + u*)/2.  FMA arith folds the average into the stages:
+    // u_half = fma(dt/2, L(u), u) next to u*, then u = fma(dt/2, L(u*), u_half)
+    // (one VALU op per cell fewer; dt/2 is exact).
     T hl, hr, r[CPL], ws[CPL];
+    const T hdt = dt * (T)0.5;
     halos<T, CPL>(w, gl, gr, c, hl, hr);
     rus_rate<T, CPL, FM, VISC>(w, hl, hr, kc, r);
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) ws[j] = madd<FM>(dt, r[j], w[j]);
+    for (int j = 0; j < CPL; ++j) {
+      ws[j] = madd<FM>(dt, r[j], w[j]);
+      if constexpr (FM) w[j] = madd<true>(hdt, r[j], w[j]);
+    }
     const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
     halos<T, CPL>(ws, gls, grs, c, hl, hr);
     rus_rate<T, CPL, FM, VISC>(ws, hl, hr, kc, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
-      ws[j] = madd<FM>(dt, r[j], ws[j]);
-      w[j] = (w[j] + ws[j]) / (T)2;
+      if constexpr (FM) {
+        w[j] = madd<true>(hdt, r[j], w[j]);
+      } else {
+        ws[j] = ws[j] + dt * r[j];
+        w[j] = (w[j] + ws[j]) / (T)2;
+      }
     }
     gl = w[0];
     gr = w[CPL - 1];

@@ -75,12 +75,38 @@ __device__ __forceinline__ T block_mean(const T (&s)[1 + J]) {
   return np_pairwise<T, J>(y, 0) / (T)J;
 }
 
+// Per-evaluation coefficients: theta = (F, h, b), hc = h c (fast_slow_fact,
+// lorenz.py:42), hJ = h / J (lorenz.py:98); FMA arith also folds the block
+// mean's 1/J into hc (hcJ = hc / J) and c into the fast rate (chJ = c hJ,
+// cb = c b), so no stage needs a division or the final scaling by c.
+template <typename T>
+struct TsCoef {
+  T F, hc, hJ, bb, cc, hcJ, chJ, cb;
+};
+
+template <typename T>
+__device__ __forceinline__ TsCoef<T> ts_coef(T F, T h, T bb, T cc, int J) {
+  TsCoef<T> k;
+  k.F = F;
+  k.bb = bb;
+  k.cc = cc;
+  k.hc = h * cc;
+  k.hJ = h / (T)J;
+  k.hcJ = k.hc / (T)J;
+  k.chJ = cc * k.hJ;
+  k.cb = cc * bb;
+  return k;
+}
+
 // dX_k/dt (lorenz.py:77-86) and dY_{k,j}/dt (lorenz.py:94-99).
+// REFERENCE: yb = block mean, the reference's operation order.
+// FMA: ys = block SUM, t = fma(x_{k+1} - x_{k-2}, x_{k-1}, F - X); fma(-hc/J, ys, t).
 template <typename T, bool FM>
-__device__ __forceinline__ T ts_slow(T X, T xm1, T xm2, T xp1, T F, T hc, T yb) {
+__device__ __forceinline__ T ts_slow(T X, T xm1, T xm2, T xp1, const TsCoef<T>& k, T ys) {
+  const T F = k.F, hc = k.hc, yb = ys;
   if constexpr (FM) {
     const T t = madd<true>(xp1 - xm2, xm1, F - X);
-    return madd<true>(-hc, yb, t);
+    return madd<true>(-k.hcJ, ys, t);
   } else {
     T t = -X;
     t = t - (xm1 * xm2 - xm1 * xp1);
@@ -89,19 +115,29 @@ __device__ __forceinline__ T ts_slow(T X, T xm1, T xm2, T xp1, T F, T hc, T yb) 
   }
 }
 
+// REFERENCE: c (((-y) - b (y_{j+1} y_{j+2} - y_{j-1} y_{j+1})) + hJ X).
+// FMA: fma(-c b, y_{j+1} (y_{j+2} - y_{j-1}), fma(-c, y, qX)) with qX = c hJ X
+// computed once per slow variable and stage.
 template <typename T, bool FM>
-__device__ __forceinline__ T ts_fast(T y, T yp1, T yp2, T ym1, T X, T hJ, T bb, T cc) {
-  T t;
+__device__ __forceinline__ T ts_fast(T y, T yp1, T yp2, T ym1, T X, T qX, const TsCoef<T>& k) {
   if constexpr (FM) {
     const T nl = yp1 * (yp2 - ym1);
-    t = madd<true>(hJ, X, -y);
-    t = madd<true>(-bb, nl, t);
+    return madd<true>(-k.cb, nl, madd<true>(-k.cc, y, qX));
   } else {
-    t = -y;
-    t = t - bb * (yp1 * yp2 - ym1 * yp1);
-    t = t + hJ * X;
+    T t = -y;
+    t = t - k.bb * (yp1 * yp2 - ym1 * yp1);
+    t = t + k.hJ * X;
+    return t * k.cc;
   }
-  return t * cc;
+}
+
+// FMA arith's block sum (REFERENCE: block_mean).
+template <typename T, int J>
+__device__ __forceinline__ T block_sum(const T (&s)[1 + J]) {
+  T y[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) y[j] = s[1 + j];
+  return np_pairwise<T, J>(y, 0);
 }
 
 // One classical RK4 stage over the lane's SPL slow variables k = sub*SPL + a
@@ -117,7 +153,7 @@ __device__ __forceinline__ T ts_fast(T y, T yp1, T yp2, T ym1, T X, T hJ, T bb, 
 // L = K/SPL lanes, before anything is written.
 template <typename T, int J, bool FM, int SPL, int STAGE>
 __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + J], T (&base)[SPL][1 + J],
-                                         T (&acc)[SPL][1 + J], T cst, T F, T hc, T hJ, T bb, T cc, const TsCtx& c) {
+                                         T (&acc)[SPL][1 + J], T cst, const TsCoef<T>& kc, const TsCtx& c) {
   auto upd = [&](int a, int i, T k) {
     if constexpr (STAGE == 1) acc[a][i] = k;
     else if constexpr (STAGE == 4) acc[a][i] = acc[a][i] + k;
@@ -130,13 +166,13 @@ __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + 
 #pragma unroll
   for (int a = 0; a < SPL; ++a) {
     Xo[a] = in[a][0];
-    yb[a] = block_mean<T, J>(in[a]);
+    yb[a] = FM ? block_sum<T, J>(in[a]) : block_mean<T, J>(in[a]);
   }
   if constexpr (SPL == 1) {
     const T xm1 = __shfl(Xo[0], c.base + (c.sub + L - 1) % L, 64);
     const T xm2 = __shfl(Xo[0], c.base + (c.sub + L - 2) % L, 64);
     const T xp1 = __shfl(Xo[0], c.base + (c.sub + 1) % L, 64);
-    kX[0] = ts_slow<T, FM>(Xo[0], xm1, xm2, xp1, F, hc, yb[0]);
+    kX[0] = ts_slow<T, FM>(Xo[0], xm1, xm2, xp1, kc, yb[0]);
   } else {
     const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
     const T p1 = __shfl(Xo[SPL - 1], prev, 64);  // X_{k0-1}
@@ -147,12 +183,13 @@ __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + 
       const T xm1 = a >= 1 ? Xo[a - 1] : p1;
       const T xm2 = a >= 2 ? Xo[a - 2] : (a == 1 ? p1 : p2);
       const T xp1 = a + 1 < SPL ? Xo[a + 1] : n0;
-      kX[a] = ts_slow<T, FM>(Xo[a], xm1, xm2, xp1, F, hc, yb[a]);
+      kX[a] = ts_slow<T, FM>(Xo[a], xm1, xm2, xp1, kc, yb[a]);
     }
   }
 #pragma unroll
   for (int a = 0; a < SPL; ++a) {
     upd(a, 0, kX[a]);
+    const T qX = FM ? kc.chJ * Xo[a] : (T)0;
     const T y0 = in[a][1], y1 = in[a][1 + (1 % J)];
     T prev = in[a][J];  // old Y_{k,J-1}: the j = 0 element's left neighbour
 #pragma unroll
@@ -160,7 +197,7 @@ __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + 
       const T y = in[a][1 + j];  // elements >= j are not yet overwritten
       const T yp1 = (j + 1 < J) ? in[a][2 + j] : y0;
       const T yp2 = (j + 2 < J) ? in[a][3 + j] : ((j + 2 - J) == 0 ? y0 : y1);
-      const T k = ts_fast<T, FM>(y, yp1, yp2, prev, Xo[a], hJ, bb, cc);
+      const T k = ts_fast<T, FM>(y, yp1, yp2, prev, Xo[a], qX, kc);
       prev = y;
       upd(a, 1 + j, k);
     }
@@ -178,8 +215,8 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
   const int k0 = kq * SPL;  // this lane's first slow variable
   const T* th0 = (const T*)m.theta0;
   const T F = th0[0] + v[0], h = th0[1] + v[1], bb = th0[2] + v[2];
-  const T cc = (T)m.coupling_c;
-  const T hc = h * cc, hJ = h / (T)J;
+  const TsCoef<T> kc = ts_coef<T>(F, h, bb, (T)m.coupling_c, J);
+  const T rJ = (T)1 / (T)J;
   const T hh = (T)m.dt, h2 = hh * (T)0.5, h6 = hh / (T)6;
   const T* x0 = (const T*)m.x0;
   T x[SPL][1 + J];
@@ -195,14 +232,15 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
   const bool refmom = (m.moment_mode == 0);
   for (int n = 0; n < m.n_steps; ++n) {
     T acc[SPL][1 + J], xs[SPL][1 + J];
-    ts_stage<T, J, FM, SPL, 1>(x, xs, x, acc, h2, F, hc, hJ, bb, cc, c);
-    ts_stage<T, J, FM, SPL, 2>(xs, xs, x, acc, h2, F, hc, hJ, bb, cc, c);
-    ts_stage<T, J, FM, SPL, 3>(xs, xs, x, acc, hh, F, hc, hJ, bb, cc, c);
-    ts_stage<T, J, FM, SPL, 4>(xs, x, x, acc, h6, F, hc, hJ, bb, cc, c);
+    ts_stage<T, J, FM, SPL, 1>(x, xs, x, acc, h2, kc, c);
+    ts_stage<T, J, FM, SPL, 2>(xs, xs, x, acc, h2, kc, c);
+    ts_stage<T, J, FM, SPL, 3>(xs, xs, x, acc, hh, kc, c);
+    ts_stage<T, J, FM, SPL, 4>(xs, x, x, acc, h6, kc, c);
 #pragma unroll
     for (int a = 0; a < SPL; ++a) {
       const T X = x[a][0];
-      const T yb = refmom ? x[a][1] : block_mean<T, J>(x[a]);
+      // FMA arith: the block mean as sum * (1/J) (REFERENCE: np.mean's division)
+      const T yb = refmom ? x[a][1] : (FM ? block_sum<T, J>(x[a]) * rJ : block_mean<T, J>(x[a]));
       ob[a][0] = ob[a][0] + X;
       ob[a][1] = ob[a][1] + yb;
       ob[a][2] = madd<FM>(X, X, ob[a][2]);

@@ -57,7 +57,7 @@ def make(cfg):
     raise SystemExit(f"unknown config {cfg}")
 
 
-def run(cfg, dtype, steps=3, lanes=0, per_launch=1, spec=None):
+def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
     dev = torch.device("cuda", 0)
     op, n, beta, sq, flop, gamma = make(cfg)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
@@ -83,8 +83,9 @@ def run(cfg, dtype, steps=3, lanes=0, per_launch=1, spec=None):
     s.y, s.gamma_inv, s.prior_sqrt = y.data_ptr(), gi.data_ptr(), sqt.data_ptr()
     s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
     s.seed, s.n_steps = 5, per_launch
-    call("ipmc_pcn_sweep", C.byref(m), C.byref(s), st)  # warm-up
-    s.step0 = per_launch
+    for _ in range(warmup):  # warm-up (clocks ramp over the first launches)
+        call("ipmc_pcn_sweep", C.byref(m), C.byref(s), st)
+        s.step0 += per_launch
     torch.cuda.synchronize(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     for a, b in ev:
@@ -101,7 +102,7 @@ def run(cfg, dtype, steps=3, lanes=0, per_launch=1, spec=None):
         "ms_per_sweep": ms,
         "pcn_steps_per_s": n / (ms * 1e-3),
         "tflops_algorithmic": n * flop / (ms * 1e-3) / 1e12,
-        "accept_rate": float(acc.sum().item()) / (n * (steps + 1) * per_launch),
+        "accept_rate": float(acc.sum().item()) / (n * (steps + warmup) * per_launch),
     }
     if per_launch > 1:
         res["steps_per_launch"] = per_launch
