@@ -9,7 +9,9 @@ import os
 
 from . import _abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libipmc.so")
+# IPMC_LIB_PATH selects another build of the same library (layout experiments).
+LIB_PATH = os.environ.get("IPMC_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                           "libipmc.so")
 
 
 class IpmcError(RuntimeError):

@@ -215,6 +215,9 @@ struct Splat<f32x2> {
 constexpr int kRowRor1 = 0x121;
 constexpr int kRowRor15 = 0x12F;
 
+// (DPP movs take VALU issue slots -- 24 of the 224 instructions of a d=40
+// RK4 step at LPC 4 -- but moving these halos to ds_bpermute measured 10 %
+// slower: profiles/r1/halo_dpp_vs_lds.txt.)
 template <int LPC, typename T>
 __device__ __forceinline__ T group_prev(T v, int lane) {
   if constexpr (LPC == 1) return v;
