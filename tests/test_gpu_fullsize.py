@@ -1,0 +1,86 @@
+"""Parity at BASELINE's full sizes (configs 4 and 5), through the C-ABI / torch ops.
+
+The oracle cannot re-run whole ensembles of this size in seconds, so each test
+runs the full ensemble on the device once and checks (a) sampled chains
+against the oracle bit for bit (forward map, Φ, sweep) and (b) the
+size-independent sharding property: the ensemble split into the per-GPU
+shards of an 8-GPU run (chain_offset = r·C/8) gives the same bits as one launch.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from test_gpu_parity import _np, _sweep_device, _sweep_oracle, _t  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return torch.device("cuda", 0)
+
+
+def _device_phi(op, U0, y, ginv, dtype, dev):
+    from ip_mcmc_amd import torch_ops
+
+    return torch_ops.potential(op, _t(U0, dtype, dev), _t(y, dtype, dev), _t(ginv, dtype, dev)).cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_cfg5_gpu_share_full_length(dev, orc, dtype):
+    """Config 5 per-GPU share: Lorenz-96 d=256, 10 000 RK4 steps, 131 072 chains
+    (2^20 / 8), as the last rank's shard (global chain ids 7·2^17 ...)."""
+    from ip_mcmc_amd import Lorenz96Operator, torch_ops
+
+    op = Lorenz96Operator(256, 8.0, dt=0.005, n_steps=10000)
+    C_, off = 131072, 7 * 131072
+    rng = np.random.default_rng(55)
+    U0 = (0.05 * rng.normal(size=(C_, 256))).astype(_np(dtype)).astype(np.float64)
+    y = orc.forward(op, U0[:1])[0] + 0.1 * rng.normal(size=256)
+    ginv, sq = np.full(256, 10.0), np.ones(256)
+    idx = np.array([0, 1, 4097, 65536, C_ - 1])
+    g = torch_ops.forward(op, _t(U0, dtype, dev)).cpu().numpy()
+    assert np.array_equal(g[idx], orc.forward(op, U0[idx], _np(dtype)))
+    phi0 = _device_phi(op, U0, y, ginv, dtype, dev).astype(np.float64)
+    assert np.array_equal(phi0[idx], orc.potential(op, U0[idx], y, ginv, _np(dtype)).astype(np.float64))
+    d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.002, 41, 0, 1, dtype, dev, chain_offset=off)
+    for i in idx:
+        o = _sweep_oracle(orc, op, U0[i:i + 1], phi0[i:i + 1], y, ginv, sq, 0.002, 41, 0, 1, dtype,
+                          chain_offset=off + int(i))
+        assert np.array_equal(d["u"][i], o["u"][0]) and d["acc"][i] == o["acc"][0], (dtype, i)
+        assert d["phi"][i] == o["phi"][0], (dtype, i)
+    assert np.all(np.isfinite(d["phi"]))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_cfg4_full_ensemble_and_shards(dev, orc, dtype):
+    """Config 4: Burgers N=256, fixed dt 1e-3 x 1000, beta 0.15, all 16 384 chains
+    in one launch == the eight 2 048-chain shards of an 8-GPU run; sampled chains
+    == the oracle."""
+    from ip_mcmc_amd import BurgersOperator
+
+    op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000)
+    C_, P = 16384, 8
+    rng = np.random.default_rng(44)
+    U0 = (0.25 * rng.normal(size=(C_, 3))).astype(_np(dtype)).astype(np.float64)
+    # truth (δ1, δ2, σ0) = (0.025, -0.025, -0.02) of burgers_beta.py, as a perturbation of the prior mean
+    y = orc.forward(op, [[0.025 - 1.5, -0.025 - 0.25, -0.02 + 0.5]])[0] + 0.05 * rng.normal(size=op.q)
+    ginv, sq = np.full(op.q, 1 / 0.05), np.full(3, 0.25)
+    phi0 = _device_phi(op, U0, y, ginv, dtype, dev).astype(np.float64)
+    n = 3
+    full = _sweep_device(op, U0, phi0, y, ginv, sq, 0.15, 23, 0, n, dtype, dev)
+    assert full["acc"].sum() > 0
+    S = C_ // P
+    for r in range(P):
+        sl = slice(r * S, (r + 1) * S)
+        sh = _sweep_device(op, U0[sl], phi0[sl], y, ginv, sq, 0.15, 23, 0, n, dtype, dev, chain_offset=r * S)
+        for key in ("u", "phi", "acc", "calls"):
+            assert np.array_equal(sh[key], full[key][sl]), (r, key)
+    idx = np.sort(rng.choice(C_, 12, replace=False))
+    for i in idx:
+        o = _sweep_oracle(orc, op, U0[i:i + 1], phi0[i:i + 1], y, ginv, sq, 0.15, 23, 0, n, dtype,
+                          chain_offset=int(i))
+        assert np.array_equal(full["u"][i], o["u"][0]) and full["acc"][i] == o["acc"][0], (dtype, i)
+        assert full["phi"][i] == o["phi"][0], (dtype, i)
