@@ -354,14 +354,12 @@ class MCMCSampler:
 
     @classmethod
     def autocorr(cls, x):
-        """Normalised autocorrelation of a 1-D chain (sampler.py:43-54)."""
-        x = np.asarray(x, dtype=np.float64)
-        x_ = x - np.mean(x)
-        result = np.correlate(x_, x_, mode="full")
-        result = result[-len(x):]
-        if result[0] == 0:
-            return np.ones_like(result)
-        return result / result[0]
+        """Normalised autocorrelation of a 1-D chain (sampler.py:43-54), all
+        len(x) lags, by the ipmc_autocorr kernel (diagnostics.autocorr; ones
+        for a constant chain, as the reference)."""
+        from .diagnostics import autocorr
+
+        return autocorr(np.asarray(x, dtype=np.float64).reshape(-1))
 
 
 def _bump(counted, calls, accepts, single):

@@ -35,20 +35,11 @@ def load():
     return torch.ops.ipmc
 
 
-class _ModelHandle:
-    """An ObservationOperator's ipmc_model for (dtype, device), kept alive with its arrays."""
-
-    _cache = {}
-
-    @classmethod
-    def address(cls, op, dtype, device):
-        key = (id(op), dtype, str(device))
-        ent = cls._cache.get(key)
-        if ent is None or ent[0] is not op:
-            m, keep = op.model(dtype, device)
-            ent = (op, m, keep)
-            cls._cache[key] = ent
-        return C.addressof(ent[1])
+def _model_address(op, dtype, device):
+    """Address of op's ipmc_model for (dtype, device); the operator caches it
+    with its device arrays for its own lifetime."""
+    m, _ = op.model(dtype, device)
+    return C.addressof(m)
 
 
 def _stream(t, stream):
@@ -60,7 +51,7 @@ def pcn_sweep(op, u, phi, accepts, y, gamma_inv, prior_sqrt, beta, seed, step0, 
     """n_steps pCN (or RW) steps of every chain of u [C, k], in place; see include/ipmc.h ipmc_pcn_sweep."""
     ops = load()
     contraction = math.sqrt(1.0 - beta * beta) if proposal == "pcn" else 1.0
-    ops.pcn_sweep(u, phi, accepts, y, gamma_inv, prior_sqrt, _ModelHandle.address(op, u.dtype, u.device),
+    ops.pcn_sweep(u, phi, accepts, y, gamma_inv, prior_sqrt, _model_address(op, u.dtype, u.device),
                   float(beta), contraction, int(seed), int(chain_offset), int(step0), int(n_steps),
                   _stream(u, stream), 1 if proposal == "rw" else 0, sum_u, sum_u2)
 
@@ -69,7 +60,7 @@ def potential(op, u, y, gamma_inv, stream=None):
     """Φ(u) for u [n, k] (device tensor) -> phi [n]."""
     ops = load()
     phi = torch.empty(u.shape[0], dtype=u.dtype, device=u.device)
-    ops.potential(u, y, gamma_inv, phi, _ModelHandle.address(op, u.dtype, u.device), _stream(u, stream))
+    ops.potential(u, y, gamma_inv, phi, _model_address(op, u.dtype, u.device), _stream(u, stream))
     return phi
 
 
@@ -77,5 +68,5 @@ def forward(op, u, stream=None):
     """G(u) for u [n, k] (device tensor) -> g [n, q]."""
     ops = load()
     g = torch.empty((u.shape[0], op.q), dtype=u.dtype, device=u.device)
-    ops.forward(u, g, _ModelHandle.address(op, u.dtype, u.device), _stream(u, stream))
+    ops.forward(u, g, _model_address(op, u.dtype, u.device), _stream(u, stream))
     return g

@@ -249,6 +249,17 @@ def rusanov_rate(w, dx, arith="reference"):
     return r
 
 
+def autocorr_ref(x):
+    """MCMCSampler.autocorr (sampler.py:43-54) restated: x_ = x - mean(x),
+    np.correlate(x_, x_, 'full')[-len(x):] / r[0], all ones for r[0] == 0."""
+    x = np.asarray(x, dtype=np.float64)
+    x_ = x - np.mean(x)
+    r = np.correlate(x_, x_, mode="full")[-len(x):]
+    if r[0] == 0:
+        return np.ones_like(r)
+    return r / r[0]
+
+
 def burn_in(x, window=50, threshold=0.03):
     """len_burn_in for chains x of shape (C, n_vars, len) or (n_vars, len) (f64)."""
     x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
