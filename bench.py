@@ -178,15 +178,24 @@ def main():
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the product path) or gloo (rehearsal of the N-rank logic)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsing N ranks on a one-GPU box; needs --dist-backend gloo)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
+    if args.share_device and args.dist_backend != "gloo":
+        raise SystemExit("--share-device needs --dist-backend gloo (RCCL wants one GPU per rank)")
+    dev = torch.device("cuda", 0 if args.share_device else local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     log(f"rank {rank}/{world} on {dev}: building the problem")
     op, y = problem()
@@ -206,7 +215,24 @@ def main():
     # rate and posterior-mean state over all chains of all ranks
     from ip_mcmc_amd.shard import gather_chains
 
-    acc_all = gather_chains(w.acc.view(-1, 1), world * args.chains)
+    # (after the timed region: per-chain state u, Φ and accept counts of every
+    # rank to every rank; all_gather_into_tensor = RCCL over xGMI at N > 1)
+    torch.cuda.synchronize(w.dev)
+    barrier(world)
+    tg = time.perf_counter()
+    host = (lambda t: t.cpu()) if args.dist_backend == "gloo" else (lambda t: t)
+    u_all = gather_chains(host(w.u), world * args.chains)
+    phi_all = gather_chains(host(w.phi.view(-1, 1)), world * args.chains)
+    acc_all = gather_chains(host(w.acc.view(-1, 1)), world * args.chains)
+    torch.cuda.synchronize(w.dev)
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    gather = {"ms": gather_ms, "bytes_per_rank": int(w.u.numel() * w.u.element_size() + w.phi.numel() *
+                                                     w.phi.element_size() + w.acc.numel() * 8),
+              "collective": (f"all_gather_into_tensor ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
+                             if world > 1 else "none (one rank)"),
+              "rows": int(u_all.shape[0])}
+    assert bool(torch.isfinite(phi_all).all())
+    del u_all, phi_all
     accept_rate = float(acc_all.double().sum().item()) / (world * args.chains * (args.steps + args.warmup))
 
     extra = {}
@@ -278,6 +304,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "accept_rate": accept_rate,
+            "final_gather": gather,
             "extra": extra,
         }
         print(json.dumps(line))
