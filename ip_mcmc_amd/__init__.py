@@ -33,7 +33,7 @@ from .forward import (
     ObservationOperator,
     TwoScaleLorenz96Operator,
 )
-from .rng import PhiloxRNG
+from .rng import PhiloxRNG, PhiloxStream
 from ._lib import IpmcError, UnsupportedOnDevice
 
 __all__ = [
@@ -62,6 +62,7 @@ __all__ = [
     "ObservationOperator",
     "TwoScaleLorenz96Operator",
     "PhiloxRNG",
+    "PhiloxStream",
     "IpmcError",
     "UnsupportedOnDevice",
 ]

@@ -55,6 +55,10 @@ class PhiloxRNG:
         return z.double().cpu().numpy().reshape(k)
 
 
+# SURVEY §8(b)'s name for the same handle
+PhiloxStream = PhiloxRNG
+
+
 def resolve_rng(rng):
     """PhiloxRNG | int seed | numpy Generator -> PhiloxRNG.
 
