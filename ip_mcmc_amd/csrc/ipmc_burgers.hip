@@ -135,30 +135,11 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   const bool cflmode = (m.dt_mode == IPMC_DT_CFL);
   bool valid = true;
   bool lane_ok = true;
-  T t = (T)0;
-  int iters = 0;
-  for (;;) {
-    T dt;
-    if (cflmode) {
-      const T mx = group_max_abs<GS>(lane_max_abs<CPL>(w, live));
-      if (!(t < tend)) break;
-      if (iters >= m.max_iter) {
-        valid = false;
-        break;
-      }
-      dt = cfl_dx / mx;
-      t = t + dt;
-    } else {
-      if (iters >= m.n_steps) break;
-      const T mx = lane_max_abs<CPL>(w, live);
-      if (!(mx * dtf <= cfl_dx)) lane_ok = false;
-      dt = dtf;
-    }
-    ++iters;
-    // SSPRK2, rusanov.py:62-74.  REFERENCE: u* = u + dt L(u); u* += dt L(u*);
-    // u = (u + u*)/2.  FMA arith folds the average into the stages:
-    // u_half = fma(dt/2, L(u), u) next to u*, then u = fma(dt/2, L(u*), u_half)
-    // (one VALU op per cell fewer; dt/2 is exact).
+  // One SSPRK2 step of size dt, rusanov.py:62-74.  REFERENCE: u* = u + dt L(u);
+  // u* += dt L(u*); u = (u + u*)/2.  FMA arith folds the average into the
+  // stages: u_half = fma(dt/2, L(u), u) next to u*, then
+  // u = fma(dt/2, L(u*), u_half) (one VALU op per cell fewer; dt/2 is exact).
+  auto step = [&](T dt) {
     T hl, hr, r[CPL], ws[CPL];
     const T hdt = dt * (T)0.5;
     halos<T, CPL>(w, gl, gr, c, hl, hr);
@@ -182,6 +163,32 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
     }
     gl = w[0];
     gr = w[CPL - 1];
+  };
+  if (cflmode) {
+    // dt = cfl dx / max|w| over the group each step, while t < t_end (the
+    // reference's overshooting loop, rusanov.py:40-45, 102-109)
+    T t = (T)0;
+    int iters = 0;
+    for (;;) {
+      const T mx = group_max_abs<GS>(lane_max_abs<CPL>(w, live));
+      if (!(t < tend)) break;
+      if (iters >= m.max_iter) {
+        valid = false;
+        break;
+      }
+      const T dt = cfl_dx / mx;
+      t = t + dt;
+      ++iters;
+      step(dt);
+    }
+  } else {
+    // fixed dt: a uniform trip count, and a per-lane CFL guard reduced once
+    const int n = m.n_steps;
+    for (int it = 0; it < n; ++it) {
+      const T mx = lane_max_abs<CPL>(w, live);
+      if (!(mx * dtf <= cfl_dx)) lane_ok = false;
+      step(dtf);
+    }
   }
   if (!cflmode) {
     // the group is valid iff every live lane kept max|w| dt <= cfl dx
