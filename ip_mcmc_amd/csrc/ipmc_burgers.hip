@@ -32,13 +32,29 @@ __device__ __forceinline__ T rus_flux_ref(T a, T b) {
   return favg - (half * sp) * (b - a);
 }
 
+// max(|a|, |b|) as ONE v_max with abs source modifiers.  fmax(fabs, fabs) in
+// C++ compiles to a canonicalising v_max per operand plus the max (the compiler
+// cannot prove the DPP-moved and loop-carried values canonical), i.e. 3 VALU
+// ops.  The hardware max is IEEE maxNum, the same value as C fmax for every
+// input these kernels produce (no signalling NaNs); the oracle uses fmax.
+__device__ __forceinline__ double max_abs(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float max_abs(float a, float b) {
+  float r;
+  asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // FMA arith: the flux pre-scaled by 1/(−dx), F̃ = fma(c2·s, b−a, c1·(a²+b²))
 // with c1 = ¼/(−dx), c2 = −½/(−dx), so dudt = F̃_{i+½} − F̃_{i−½} needs no
 // division (7 VALU ops per interface).  max is fmax: equal to the reference's
 // max for every non-NaN pair.
 template <typename T>
 __device__ __forceinline__ T rus_flux_fm(T a, T b, T c1, T c2) {
-  const T sp = __builtin_fmax(__builtin_fabs(a), __builtin_fabs(b));
+  const T sp = max_abs(a, b);
   const T sq = madd<true>(b, b, a * a);
   return madd<true>(c2 * sp, b - a, c1 * sq);
 }
@@ -60,7 +76,7 @@ __device__ __forceinline__ T lane_max_abs(const T (&w)[CPL], bool live) {
   T m = (T)0;
   if (live) {
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) m = __builtin_fmax(m, __builtin_fabs(w[j]));
+    for (int j = 0; j < CPL; ++j) m = max_abs(m, w[j]);  // m >= 0
   }
   return m;
 }
