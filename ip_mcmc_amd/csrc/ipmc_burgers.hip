@@ -64,7 +64,7 @@ __device__ __forceinline__ T group_max_abs(T m) {
 #pragma unroll
   for (int off = GS / 2; off >= 1; off >>= 1) {
     const T o = __shfl_xor(m, off, 64);
-    m = __builtin_fmax(o, m);
+    m = __builtin_fmax(o, m);  // (max_abs here measured slower: cfg 4 CFL 0.47 -> 0.51 ms)
   }
   return m;
 }
