@@ -299,6 +299,12 @@ class MCMCSampler:
             if sink is not None and (slot == buf_len - 1 or i == n_samples - 1):
                 blk = samples[:, : slot + 1, :].double().cpu().numpy()
                 sink.write(i - slot, blk[0] if single else blk)
+        # the host copy of the samples goes to page-locked memory (~57 GB/s
+        # instead of ~5 GB/s pageable on the MI355X box, profiles/r1/d2h_probe.txt);
+        # allocating it here overlaps the allocation with the queued sweeps
+        host_out = None
+        if keep == "samples" and sink is None:
+            host_out = _host_buffer(tuple(samples.shape))
         torch.cuda.synchronize(device)
         self.last_run_seconds = time.perf_counter() - t0
 
@@ -327,7 +333,8 @@ class MCMCSampler:
         if keep == "samples":
             if sink is not None:
                 return sink.close()
-            out = samples.double().cpu().numpy()
+            host_out.copy_(samples if samples.dtype == torch.float64 else samples.double())
+            out = host_out.numpy()  # shares the page-locked buffer (kept alive by the array)
             return out[0] if single else out
         if keep == "moments":
             n_post = n_samples * sample_interval
@@ -360,6 +367,18 @@ class MCMCSampler:
         from .diagnostics import autocorr
 
         return autocorr(np.asarray(x, dtype=np.float64).reshape(-1))
+
+
+# page-locked host buffers up to this size; larger sample arrays use pageable
+# memory (or stream to disk with run(sample_file=...))
+PINNED_MAX_BYTES = 8 << 30
+
+
+def _host_buffer(shape):
+    n = 8
+    for d in shape:
+        n *= int(d)
+    return torch.empty(shape, dtype=torch.float64, pin_memory=n <= PINNED_MAX_BYTES)
 
 
 def _bump(counted, calls, accepts, single):
