@@ -51,6 +51,9 @@ def main():
     rec["effective_clock_GHz"] = clock_ghz
     rec["valu_instr_per_wave"] = rec["SQ_INSTS_VALU"] / rec["SQ_WAVES"]
     rec["valu_issue_utilisation"] = rec["SQ_INSTS_VALU"] * cpi / (1024 * ns * clock_ghz)
+    # the same from the activity counter, no per-instruction cost assumed:
+    # VALU-active quad-cycles summed over waves / (SIMDs x kernel cycles)
+    rec["valu_busy_from_active_cycles"] = rec["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * ns * clock_ghz)
     rec["cycles_per_valu_assumed"] = cpi
     print(json.dumps(rec, indent=1))
 
