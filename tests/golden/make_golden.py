@@ -300,6 +300,37 @@ def make_linear(out):
     out["lin_phi"] = np.array([pot(u) for u in U])
 
 
+def make_constrained(out):
+    """ConstrainAccepter (accepter.py:39-55) around CountedAccepter(pCNAccepter)
+    through the reference sampler: a proposal the constraint rejects never
+    reaches the inner accepter (no call counted, no uniform drawn).  The
+    constraint is a strict box on two components, like is_valid_IC
+    (burgers_wasserstein_chain.py:47-55)."""
+    g = np.array([3.0, 1.0, 4.0, 1.0])
+    gamma = 0.5
+    y = np.array([np.dot(g, [2.0, 7.0, 1.0, 8.0]) + 0.1])
+    lo = np.array([-0.6, -np.inf, -1.0, -np.inf])
+    hi = np.array([0.6, np.inf, 1.0, np.inf])
+    seed = 4242
+
+    def is_valid(v):
+        return bool(np.all(lo < v) and np.all(v < hi))
+
+    def G(u):
+        return np.dot(g, u)
+
+    res = []
+    for chain in range(3):
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, np.array([gamma**2]), np.ones(4), 0.5, np.zeros(4), seed, chain, n_samples=30, burn_in=60,
+            interval=10, box=is_valid)
+        res.append((s, calls, accepts))
+    out["con_g"], out["con_y"], out["con_lo"], out["con_hi"] = g, y, lo, hi
+    out["con_meta"] = np.array([gamma, 0.5, seed, 30, 60, 10], dtype=np.float64)
+    out["con_samples"] = np.stack([r[0] for r in res])
+    out["con_counts"] = np.array([[r[1], r[2]] for r in res])
+
+
 def pw_linear(d_s, d_e, l):
     """The harness's step schedule, the formula of burgers_beta.py:131-147's PWLinear
     (that script cannot be imported here: it pulls in helpers.py, which needs POT)."""
@@ -511,6 +542,7 @@ def main():
     make_l96_chain(out)
     make_l96ts(out)
     make_linear(out)
+    make_constrained(out)
     make_rw(out)
     make_burgers(out)
     make_misc(out)

@@ -338,6 +338,28 @@ def test_sampler_single_chain_matches_reference_fixture(dev, golden):
         assert acc.calls == int(golden["lin_counts"][chain, 0])
 
 
+def test_sampler_constrained_chain_matches_reference_fixture(dev, golden):
+    """ConstrainAccepter(CountedAccepter(pCNAccepter), BoxConstraint) through the
+    drop-in API reproduces the reference's constrained chains (accepter.py:39-55):
+    samples, accepts and the inner accepter's calls."""
+    from ip_mcmc_amd import (BoxConstraint, ConstrainAccepter, ConstSteppCNProposer, CountedAccepter,
+                             EvolutionPotential, GaussianDistribution, LinearOperator, MCMCSampler, PhiloxRNG,
+                             pCNAccepter)
+
+    gamma, beta, seed, n_samples, burn_in, interval = golden["con_meta"]
+    pot = EvolutionPotential(LinearOperator(golden["con_g"], arith="reference"), golden["con_y"],
+                             GaussianDistribution(0, gamma**2))
+    for chain in range(3):
+        inner = CountedAccepter(pCNAccepter(pot))
+        acc = ConstrainAccepter(inner, BoxConstraint(lower=golden["con_lo"], upper=golden["con_hi"]))
+        s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))), acc,
+                        PhiloxRNG(int(seed)), chain_offset=chain)
+        out = s.run(np.zeros(4), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+        assert np.array_equal(out, golden["con_samples"][chain])
+        assert inner.calls == int(golden["con_counts"][chain, 0])
+        assert inner.accepts == int(golden["con_counts"][chain, 1])
+
+
 def test_sampler_l96_chain_matches_reference_fixture(dev, golden):
     from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, Lorenz96Operator,
                              MCMCSampler, PhiloxRNG, pCNAccepter)

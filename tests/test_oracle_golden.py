@@ -264,3 +264,31 @@ def test_burn_in_oracle_matches_reference(orc, golden):
         assert orc.burn_in(golden[f"bi_x_{i}"]) == int(golden[f"bi_out_{i}"]), i
     assert np.array_equal(orc.burn_in(golden["bi_batch_x"]), golden["bi_batch_out"])
     assert len(set(golden["bi_batch_out"].tolist())) > 5, "fixture exercises too few outcomes"
+
+
+def test_constrained_chain_matches_reference_sampler(orc, golden):
+    """ConstrainAccepter(CountedAccepter(pCNAccepter)) through the reference sampler
+    (accepter.py:39-55): box-rejected proposals neither call the inner accepter nor
+    draw its uniform; the oracle's box reproduces samples, accepts and calls."""
+    gamma, beta, seed, n_samples, burn_in, interval = golden["con_meta"]
+    op = LinearOperator(golden["con_g"], arith="reference")
+    n_chains, y = 3, golden["con_y"]
+    U = np.zeros((n_chains, 4))
+    ginv = np.full(1, 1.0 / gamma)
+    phi = orc.potential(op, U, y, ginv)
+    acc = np.zeros(n_chains, dtype=np.int64)
+    calls = np.zeros(n_chains, dtype=np.int64)
+    box = (golden["con_lo"], golden["con_hi"], None)
+    step = 0
+    nb = max(0, int(burn_in) - int(interval))
+    orc.pcn_sweep(op, U, phi, y, ginv, np.ones(4), beta, int(seed), step, nb, accepts=acc, calls=calls, box=box)
+    step += nb
+    samples = np.zeros((n_chains, int(n_samples), 4))
+    for i in range(int(n_samples)):
+        orc.pcn_sweep(op, U, phi, y, ginv, np.ones(4), beta, int(seed), step, int(interval), accepts=acc,
+                      calls=calls, box=box)
+        step += int(interval)
+        samples[:, i] = U
+    np.testing.assert_array_equal(samples, golden["con_samples"])
+    assert np.array_equal(calls, golden["con_counts"][:, 0])
+    assert np.array_equal(acc, golden["con_counts"][:, 1])
