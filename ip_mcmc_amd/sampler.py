@@ -274,10 +274,14 @@ class MCMCSampler:
         if keep == "samples":
             if sample_file is not None:
                 sink = NpySampleSink(sample_file, (n_samples, k) if single else (n_chains, n_samples, k))
-                # device staging buffer of <= ~256 MiB between flushes
+                # device staging buffers of <= ~256 MiB between flushes
                 auto = max(1, (1 << 28) // max(1, n_chains * k * 8))
                 buf_len = max(1, min(n_samples, int(flush_every) if flush_every else auto))
-            samples = torch.empty((n_chains, buf_len, k), dtype=td, device=device)
+                writer = _StreamingWriter(sink, (n_chains, buf_len, k), td, device, 2 if n_samples > buf_len else 1,
+                                          single)
+                samples = writer.buffer
+            else:
+                samples = torch.empty((n_chains, buf_len, k), dtype=td, device=device)
         elif keep == "moments":
             sums = (
                 torch.zeros((n_chains, k), dtype=torch.float64, device=device),
@@ -297,8 +301,9 @@ class MCMCSampler:
             if sample_interval == 0 and samples is not None:
                 launch(0, samples[:, slot, :])
             if sink is not None and (slot == buf_len - 1 or i == n_samples - 1):
-                blk = samples[:, : slot + 1, :].double().cpu().numpy()
-                sink.write(i - slot, blk[0] if single else blk)
+                samples = writer.flush(i - slot, slot + 1)
+        if sink is not None:
+            writer.finish()
         # the host copy of the samples goes to page-locked memory (~57 GB/s
         # instead of ~5 GB/s pageable on the MI355X box, profiles/r1/d2h_probe.txt);
         # allocating it here overlaps the allocation with the queued sweeps
@@ -372,6 +377,61 @@ class MCMCSampler:
 # page-locked host buffers up to this size; larger sample arrays use pageable
 # memory (or stream to disk with run(sample_file=...))
 PINNED_MAX_BYTES = 8 << 30
+
+
+class _StreamingWriter:
+    """Double-buffered sample streaming for run(sample_file=...): while the
+    sweeps fill one device staging buffer, the previous one goes to page-locked
+    host memory on a copy stream and from there to the .npy file, so the GPU
+    does not wait for PCIe or the disk (one buffer when everything fits in it)."""
+
+    def __init__(self, sink, shape, dtype, device, n_buf, single):
+        self.sink, self.single, self.device = sink, single, device
+        self.dev = [torch.empty(shape, dtype=dtype, device=device) for _ in range(n_buf)]
+        nbytes = torch.empty((), dtype=dtype).element_size()
+        for d in shape:
+            nbytes *= int(d)
+        pin = nbytes <= PINNED_MAX_BYTES
+        self.host = [torch.empty(shape, dtype=dtype, pin_memory=pin) for _ in range(n_buf)]
+        self.done = [None] * n_buf  # D2H of buffer b finished
+        self.pending = []  # (b, first sample index, samples) copied or in flight, not yet written
+        self.copy_stream = torch.cuda.Stream(device=device)
+        self.cur = 0
+
+    @property
+    def buffer(self):
+        return self.dev[self.cur]
+
+    def flush(self, i0, nb):
+        """The current buffer holds samples i0 .. i0+nb-1: start its copy to the
+        host, write the block before it to the file, and return the buffer the
+        next sweeps write into."""
+        b = self.cur
+        filled = torch.cuda.Event()
+        filled.record(torch.cuda.current_stream(self.device))
+        self.copy_stream.wait_event(filled)
+        with torch.cuda.stream(self.copy_stream):
+            self.host[b][:, :nb].copy_(self.dev[b][:, :nb], non_blocking=True)
+            self.done[b] = torch.cuda.Event()
+            self.done[b].record(self.copy_stream)
+        self.pending.append((b, i0, nb))
+        if len(self.pending) == len(self.dev):
+            self._write_oldest()
+        self.cur = (b + 1) % len(self.dev)
+        if self.done[self.cur] is not None:
+            # the sweeps must not overwrite a buffer its D2H is still reading
+            torch.cuda.current_stream(self.device).wait_event(self.done[self.cur])
+        return self.dev[self.cur]
+
+    def _write_oldest(self):
+        b, i0, nb = self.pending.pop(0)
+        self.done[b].synchronize()
+        blk = self.host[b][:, :nb].numpy()
+        self.sink.write(i0, blk[0] if self.single else blk)
+
+    def finish(self):
+        while self.pending:
+            self._write_oldest()
 
 
 def _host_buffer(shape):
