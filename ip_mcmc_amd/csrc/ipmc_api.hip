@@ -69,32 +69,51 @@ static bool l96_has(int D, int dtype, int lpc, int cpl) {
   return l96_has_f32(D, lpc, cpl);
 }
 
-// Layout choice for Lorenz-96 (lanes per chain, chains per lane group).
-// fp32 packs two chains per lane group (every FLOP a v_pk_*_f32).  The lane
-// count is the smallest that keeps M = d/LPC <= 10 components per lane (6
-// live arrays of M fit ~3 waves/SIMD without spills), raised while the
-// ensemble would leave SIMDs without 2 waves (1024 SIMDs: 131072 lanes),
-// as long as M stays >= 4 (the halo exchange is 3 values per RHS).
+// Layout choice for Lorenz-96 (lanes per chain LPC, chains per lane group CPL),
+// from the layout scans of profiles/r1/lanes_scan_*.txt and lanes_layout_rule.txt:
+//  1. the fewest lanes per chain whose halos go by DPP (LPC 1, 2, 4, 16) that
+//     still gives every SIMD one wave (kWaveLanes lanes), packed fp32 (CPL 2)
+//     first; more lanes only add halo work, fewer leave SIMDs idle.  With more
+//     than 16 components per lane the next layout (LPC 2 -> 4, <= 4 waves)
+//     measured as fast or faster (fp32 d=40: 1.80 vs 1.88 ms);
+//  2. else any compiled layout reaching one wave (LPC 8: halos through LDS);
+//  3. else (an ensemble below one wave per SIMD) the most lanes per chain
+//     that keep >= 4 components per lane.
 static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
-  static const int cands[5] = {1, 2, 4, 8, 16};
-  cpl = (dtype == IPMC_F32) ? 2 : 1;
-  const int64_t groups = (n_chains + cpl - 1) / cpl;
-  lpc = 0;
-  for (int i = 0; i < 5; ++i) {
-    const int l = cands[i];
-    if (!l96_has(D, dtype, l, cpl)) continue;
-    if (lpc == 0) lpc = l;  // smallest compiled
-    if (D / l <= 10) {
+  constexpr int64_t kWaveLanes = 65536;  // 256 CUs x 4 SIMDs x 64 lanes
+  static const int dpp[4] = {1, 2, 4, 16};
+  static const int all[5] = {1, 2, 4, 8, 16};
+  const int ncpl = dtype == IPMC_F32 ? 2 : 1;
+  const int cpls[2] = {ncpl, 1};
+  auto ok = [&](int l, int c) { return D % l == 0 && D / l >= 2 && l96_has(D, dtype, l, c); };
+  for (int ci = 0; ci < ncpl; ++ci) {
+    const int c = cpls[ci];
+    const int64_t groups = (n_chains + c - 1) / c;
+    for (int i = 0; i < 4; ++i) {
+      int l = dpp[i];
+      if (!ok(l, c) || groups * l < kWaveLanes) continue;
+      if (D / l > 16 && l <= 2 && ok(2 * l, c) && groups * 2 * l <= 4 * kWaveLanes) l *= 2;
       lpc = l;
-      break;
+      cpl = c;
+      return;
     }
-    lpc = l;  // keep the largest compiled while M > 10
   }
-  for (int i = 0; i < 5 && lpc; ++i) {
-    const int l = cands[i];
-    if (l <= lpc || !l96_has(D, dtype, l, cpl)) continue;
-    if (groups * lpc >= 131072 || D / l < 4) break;
-    lpc = l;
+  for (int ci = 0; ci < ncpl; ++ci) {
+    const int c = cpls[ci];
+    const int64_t groups = (n_chains + c - 1) / c;
+    for (int i = 0; i < 5; ++i) {
+      if (ok(all[i], c) && groups * all[i] >= kWaveLanes) {
+        lpc = all[i];
+        cpl = c;
+        return;
+      }
+    }
+  }
+  lpc = 0;
+  for (int ci = ncpl - 1; ci >= 0 && !lpc; --ci) {  // one chain per lane group first
+    cpl = cpls[ci];
+    for (int i = 0; i < 5; ++i)
+      if (ok(all[i], cpl) && (D / all[i] >= 4 || !lpc)) lpc = all[i];
   }
 }
 

@@ -173,6 +173,23 @@ def test_auto_layout(h):
     assert h.ipmc_auto_layout(None, _abi.F64, 1) == 0
 
 
+# (dim, dtype, chains) -> cpl * 100 + lpc: the measured-fastest layout, or one
+# within 4 % of it, of profiles/r1/lanes_layout_rule.txt
+LAYOUT_TABLE = [
+    (8, "f64", 16384, 104), (8, "f64", 65536, 101), (8, "f32", 16384, 104), (8, "f32", 65536, 202),
+    (16, "f64", 16384, 104), (16, "f64", 65536, 101), (16, "f32", 16384, 104), (16, "f32", 65536, 202),
+    (40, "f64", 8192, 108), (40, "f64", 16384, 104), (40, "f64", 32768, 104), (40, "f64", 65536, 104),
+    (40, "f32", 8192, 108), (40, "f32", 16384, 104), (40, "f32", 32768, 204), (40, "f32", 65536, 204),
+    (80, "f64", 16384, 104), (80, "f64", 65536, 104), (80, "f32", 16384, 216), (80, "f32", 65536, 204),
+]
+
+
+@pytest.mark.parametrize("dim,dt,chains,want", LAYOUT_TABLE)
+def test_auto_layout_follows_the_layout_scans(h, dim, dt, chains, want):
+    m = _model(dim=dim, k=dim, q=dim)
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F64 if dt == "f64" else _abi.F32, chains) == want
+
+
 def test_python_layer_raises_with_the_library_message():
     from ip_mcmc_amd._lib import IpmcError, call
 

@@ -8,7 +8,8 @@ cfg4full Burgers as cfg4 with all 16 384 chains on one GPU
 cfg4cfl  Burgers N=256, reference CFL time stepping, 2 048 chains
 cfg4visc Burgers N=256 with viscosity nu = 1e-3 (central differences), fixed dt 1e-3 x 1000, 2 048 chains
 cfg5     Lorenz-96 d=256, 10 000 RK4 steps, 131 072 chains (= 2^20 / 8 GPUs)
-l96xN    the headline problem with N = 1, 64 or 1024 chains (speculative sweeps)
+l96xN    the headline problem with N chains (N = 1, 64, 1024: speculative sweeps; 8192..65536: the
+         per-GPU share of a strong-scaled 65 536-chain run)
 ts6      two-scale Lorenz-96 K=6 J=4 (the thesis problem, lorenz_mcmc.py:87-88), T=20 (4 000 RK4 steps), 65 536 chains
 ts36     two-scale Lorenz-96 K=36 J=10, 2 000 RK4 steps of 0.002, 16 384 chains
 """
@@ -50,7 +51,7 @@ def make(cfg):
     if cfg == "ts36":
         op = TwoScaleLorenz96Operator(K=36, J=10, dt=0.002, n_steps=2000, moments="mean")
         return op, 16384, 0.5, np.sqrt([10.0, 1.0, 10.0]), 45 * 396 * 2000, 0.5
-    if cfg in ("l96x1", "l96x64", "l96x1024"):
+    if cfg.startswith("l96x"):
         # the headline problem with few chains (the reference runs one): speculation territory
         op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=2000)
         return op, int(cfg[4:]), 0.2, np.ones(40), 30 * 40 * 2000, 0.1
@@ -112,6 +113,7 @@ def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
         res["spec_width"] = spec
     if isinstance(op, Lorenz96Operator):
         res["lanes_per_chain"] = lib().ipmc_auto_lanes(C.byref(m), adt, n)
+        res["auto_layout"] = lib().ipmc_auto_layout(C.byref(m), adt, n)  # chains_per_lane * 100 + lanes
     print(json.dumps(res), flush=True)
 
 
