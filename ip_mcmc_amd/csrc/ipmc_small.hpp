@@ -168,18 +168,53 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
 // the chain by up to S steps in one forward-map latency.
 constexpr int kSpecBlock = 256;
 constexpr int kSpecKMax = 8;
+// linear G: A [q, k], y [q] and 1/γ [q] staged in LDS when q (k + 2) fits
+constexpr int kSpecLinLds = 1024;
+
+// Linear Φ with A, y, 1/γ from LDS and θ0 from registers: the operations and
+// order of small_potential<LINEAR> (same bits), without a global-memory round
+// trip per element in every speculative round.
+template <typename T, bool FM>
+__device__ __forceinline__ T lin_potential_staged(const T* As, const T* ys, const T* gs, const T (&th0)[kSpecKMax],
+                                                  int q, int k, const T* v, int vstride) {
+  T s = (T)0;
+  for (int i = 0; i < q; ++i) {
+    T acc = (T)0;
+#pragma unroll
+    for (int j = 0; j < kSpecKMax; ++j)
+      if (j < k) acc = madd<FM>(As[i * k + j], th0[j] + v[j * vstride], acc);
+    const T r = (ys[i] - acc) * gs[i];
+    s = madd<FM>(r, r, s);
+  }
+  return (T)0.5 * s;
+}
 
 template <typename T, int MODEL, bool FM, int S>
 __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model m, const ipmc_sweep s) {
   __shared__ T vpark[kSpecKMax * kSpecBlock];
+  __shared__ T lin_c[MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1];
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int sub = t & (S - 1);
   const int gbase = lane & ~(S - 1);
   const unsigned long long gmask = (S == 64) ? ~0ull : ((1ull << S) - 1);
   const int64_t chain = ((int64_t)blockIdx.x * kSpecBlock + t) / S;
-  if (chain >= s.n_chains) return;  // whole groups leave together
   const int k = m.k;
+  // per-problem constants, read once per launch instead of once per round
+  bool staged = false;
+  if constexpr (MODEL == IPMC_MODEL_LINEAR) {
+    const int q = m.q, nA = m.q * k;
+    staged = q * (k + 2) <= kSpecLinLds;
+    if (staged) {
+      for (int i = t; i < nA; i += kSpecBlock) lin_c[i] = ((const T*)m.A)[i];
+      for (int i = t; i < q; i += kSpecBlock) {
+        lin_c[nA + i] = ((const T*)s.y)[i];
+        lin_c[nA + q + i] = ((const T*)s.gamma_inv)[i];
+      }
+    }
+    __syncthreads();  // every thread of the block, before any leaves
+  }
+  if (chain >= s.n_chains) return;  // whole groups leave together
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
   T* __restrict__ u = (T*)s.u + chain * k;
   const T* sq = (const T*)s.prior_sqrt;
@@ -191,9 +226,19 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   T* phi = (T*)s.phi;
   T* v = vpark + t;                       // this lane's proposal, v[j * kSpecBlock]
   const T* vgroup = vpark + (t - sub);    // lane 0 of the group
-  T ur[kSpecKMax];
+  const T* rs = (const T*)s.reg_scale;
+  T ur[kSpecKMax], sqr[kSpecKMax], lor[kSpecKMax], hir[kSpecKMax], offr[kSpecKMax], rsr[kSpecKMax], th0r[kSpecKMax];
 #pragma unroll
-  for (int j = 0; j < kSpecKMax; ++j) ur[j] = j < k ? u[j] : (T)0;
+  for (int j = 0; j < kSpecKMax; ++j) {
+    const bool in = j < k;
+    ur[j] = in ? u[j] : (T)0;
+    sqr[j] = in ? sq[j] : (T)0;
+    lor[j] = (in && lo) ? lo[j] : (T)0;
+    hir[j] = (in && hi) ? hi[j] : (T)0;
+    offr[j] = (in && off) ? off[j] : (T)0;
+    rsr[j] = (in && rs) ? rs[j] : (T)0;
+    th0r[j] = (in && MODEL == IPMC_MODEL_LINEAR) ? ((const T*)m.theta0)[j] : (T)0;
+  }
   T phu = phi[chain];
   int64_t nacc = 0, ncalls = 0;
   int64_t st = 0;
@@ -212,17 +257,33 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       for (int j = 0; j < kSpecKMax; ++j) {
         if (j < k) {
           if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
-          const T w = sq[j] * (T)((j & 1) ? z1 : z0);
+          const T w = sqr[j] * (T)((j & 1) ? z1 : z0);
           const T vj = propose_one<T>(rw, ur[j], w, cs, bs);
           v[j * kSpecBlock] = vj;
-          const T tb = vj + (off ? off[j] : (T)0);
-          if (lo && !(lo[j] < tb)) ok = false;
-          if (hi && !(tb < hi[j])) ok = false;
+          const T tb = vj + offr[j];  // + 0 when there is no offset: the same bits as vj
+          if (lo && !(lor[j] < tb)) ok = false;
+          if (hi && !(tb < hir[j])) ok = false;
         }
       }
       if (ok) {
-        phv = small_potential<T, MODEL, FM>(m, v, kSpecBlock, (const T*)s.y, (const T*)s.gamma_inv);
-        if (s.reg_scale) phv = phv + small_regularizer<T, FM>(k, (const T*)s.reg_scale, v, kSpecBlock);
+        if constexpr (MODEL == IPMC_MODEL_LINEAR) {
+          const int nA = m.q * k;
+          phv = staged ? lin_potential_staged<T, FM>(lin_c, lin_c + nA, lin_c + nA + m.q, th0r, m.q, k, v, kSpecBlock)
+                       : small_potential<T, MODEL, FM>(m, v, kSpecBlock, (const T*)s.y, (const T*)s.gamma_inv);
+        } else {
+          phv = small_potential<T, MODEL, FM>(m, v, kSpecBlock, (const T*)s.y, (const T*)s.gamma_inv);
+        }
+        if (rs) {
+          T r2 = (T)0;  // small_regularizer's order
+#pragma unroll
+          for (int j = 0; j < kSpecKMax; ++j) {
+            if (j < k) {
+              const T tj = rsr[j] * v[j * kSpecBlock];
+              r2 = madd<FM>(tj, tj, r2);
+            }
+          }
+          phv = phv + (T)0.5 * r2;
+        }
         acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
       }
     }

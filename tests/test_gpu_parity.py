@@ -653,7 +653,12 @@ def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
     from ip_mcmc_amd import LinearOperator, Lorenz63Operator
 
     rng = np.random.default_rng(23)
+    # linear G: A, y, 1/γ staged in LDS (q (k + 2) <= 1024: the first three) or read
+    # from global memory (the last, q = 300)
     ops = [LinearOperator(rng.normal(size=(3, 5)), rng.normal(size=5), arith="reference"),
+           LinearOperator(rng.normal(size=(4, 3)), rng.normal(size=3)),
+           LinearOperator(0.1 * rng.normal(size=(100, 8)), rng.normal(size=8)),
+           LinearOperator(0.05 * rng.normal(size=(300, 6)), rng.normal(size=6)),
            Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=200),
            Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=200, arith="reference")]
     n = 37
@@ -661,7 +666,8 @@ def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
     for op in ops:
         U0, phi0, y, ginv, sq = _problem(op, 45, dtype, orc, seed=2)
         box = (np.full(op.k, -1.5), None, None)
-        for kw in (dict(), dict(box=box), dict(sched=sched), dict(want_sums=True)):
+        box2 = (np.full(op.k, -1.2), np.full(op.k, 1.4), np.full(op.k, 0.1))
+        for kw in (dict(), dict(box=box), dict(box=box2), dict(sched=sched), dict(want_sums=True)):
             o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, **kw)
             assert 0 < o["acc"].sum() < 45 * n
             for w in (1, 0, 2, 8, 64):
