@@ -46,3 +46,20 @@ def test_f32_samples_come_back_as_float64():
     out = s.run(np.zeros((3, 4)), n_samples=5, burn_in=4, sample_interval=2)
     assert out.dtype == np.float64 and out.shape == (3, 5, 4)
     assert np.array_equal(out, out.astype(np.float32).astype(np.float64))  # f32 values, widened
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("flush", [1, 3, 10, 25])
+def test_streaming_to_npy_equals_in_memory(tmp_path, dtype, flush):
+    """run(sample_file=...) through the double-buffered writer (one buffer when
+    every sample fits, a partial last block otherwise) = the in-memory samples,
+    for one chain ((n, k) file, the reference's layout) and for a stack."""
+    for u0 in (np.zeros(4), np.zeros((7, 4))):
+        s1, _ = _sampler(dtype)
+        mem = s1.run(u0, n_samples=10, burn_in=4, sample_interval=2)
+        s2, _ = _sampler(dtype)
+        path = str(tmp_path / f"s_{flush}_{np.dtype(dtype).name}_{u0.ndim}.npy")
+        f = s2.run(u0, n_samples=10, burn_in=4, sample_interval=2, sample_file=path, flush_every=flush)
+        assert f.shape == mem.shape and f.dtype == np.float64
+        assert np.array_equal(np.asarray(f), mem)
+        assert np.array_equal(np.load(path), mem)
