@@ -77,8 +77,11 @@ static bool l96_has(int D, int dtype, int lpc, int cpl) {
 //     than 16 components per lane the next layout (LPC 2 -> 4, <= 4 waves)
 //     measured as fast or faster (fp32 d=40: 1.80 vs 1.88 ms);
 //  2. else any compiled layout reaching one wave (LPC 8: halos through LDS);
-//  3. else (an ensemble below one wave per SIMD) the most lanes per chain
-//     that keep >= 4 components per lane.
+//  3. else (an ensemble below one wave per SIMD, where the speculative sweep
+//     fills lanes with slots) the most DPP lanes per chain that keep >= 4
+//     components per lane: a chain's RK4 step is then a latency chain, and
+//     LDS halos made it 1.6x slower (d=40 at 1 / 64 / 1 024 chains: LPC 4
+//     0.050 / 0.050 / 0.054 ms per step vs LPC 8 0.080 / 0.084 / 0.087).
 static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   constexpr int64_t kWaveLanes = 65536;  // 256 CUs x 4 SIMDs x 64 lanes
   static const int dpp[4] = {1, 2, 4, 16};
@@ -112,8 +115,10 @@ static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   lpc = 0;
   for (int ci = ncpl - 1; ci >= 0 && !lpc; --ci) {  // one chain per lane group first
     cpl = cpls[ci];
-    for (int i = 0; i < 5; ++i)
-      if (ok(all[i], cpl) && (D / all[i] >= 4 || !lpc)) lpc = all[i];
+    for (int i = 0; i < 4; ++i)
+      if (ok(dpp[i], cpl) && D / dpp[i] >= 4) lpc = dpp[i];
+    for (int i = 0; i < 5 && !lpc; ++i)
+      if (ok(all[i], cpl)) lpc = all[i];
   }
 }
 

@@ -181,6 +181,8 @@ LAYOUT_TABLE = [
     (40, "f64", 8192, 108), (40, "f64", 16384, 104), (40, "f64", 32768, 104), (40, "f64", 65536, 104),
     (40, "f32", 8192, 108), (40, "f32", 16384, 104), (40, "f32", 32768, 204), (40, "f32", 65536, 204),
     (80, "f64", 16384, 104), (80, "f64", 65536, 104), (80, "f32", 16384, 216), (80, "f32", 65536, 204),
+    # below one wave per SIMD (speculative sweeps): DPP halos (profiles/r1/l96_small_layouts.jsonl)
+    (40, "f64", 1, 104), (40, "f64", 64, 104), (40, "f64", 1024, 104), (40, "f32", 1, 104), (40, "f32", 1024, 104),
 ]
 
 
