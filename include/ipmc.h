@@ -120,7 +120,8 @@ typedef struct ipmc_sweep {
   int32_t spec_width;       /* speculative steps per round (0 = auto, 1 = off; a power of two): spec_width lane
                                groups per chain each evaluate one of the next steps from the current state, the
                                first acceptance ends the round -- results identical, small ensembles run faster.
-                               Lorenz-63 / linear (k <= 8), Lorenz-96 (spec_width * lanes_per_chain <= 64),
+                               Lorenz-63 / linear (k <= 8), Lorenz-96 (spec_width * lanes_per_chain <= 64, or = 256:
+                               the slots of one chain over the 4 waves of a block),
                                Burgers (spec_width * lanes of a chain <= 64), two-scale Lorenz-96 (any width
                                with spec_width * K <= 64). */
   int64_t n_chains;

@@ -337,15 +337,20 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
       // speculation (l96_spec_kernel): spec_width slots of lpc lanes per chain,
       // auto = the widest keeping the ensemble within one wave per SIMD
       int spec = s->spec_width;
-      if (spec < 0 || spec > 64 || (spec & (spec - 1)))
-        return fail(IPMC_ERR_UNSUPPORTED, "spec_width must be a power of two <= 64");
+      if (spec < 0 || spec > kL96SpecBlockLanes || (spec & (spec - 1)))
+        return fail(IPMC_ERR_UNSUPPORTED, "spec_width must be a power of two <= 256");
       if (spec == 0) {
         spec = 1;
-        if (s->n_steps > 1 && s->chains_per_lane != 2)
+        if (s->n_steps > 1 && s->chains_per_lane != 2) {
           while (spec * 2 * lpc <= 64 && s->n_chains * (int64_t)lpc * spec * 2 <= 65536) spec *= 2;
+          // a whole block of slots per chain (4 waves on the CU's 4 SIMDs) while
+          // the ensemble stays within one wave per SIMD
+          if (spec * lpc == 64 && s->n_chains * (int64_t)kL96SpecBlockLanes <= 65536) spec = kL96SpecBlockLanes / lpc;
+        }
       }
       if (spec > 1) {
-        if (spec * lpc > 64) return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: spec_width * lanes_per_chain must be <= 64");
+        if (spec * lpc > 64 && spec * lpc != kL96SpecBlockLanes)
+          return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: spec_width * lanes_per_chain must be <= 64 or 256");
         if (cpl == 2) {
           if (s->chains_per_lane == 2)
             return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: speculation runs one chain per lane group");

@@ -7,6 +7,10 @@
 
 namespace ipmc {
 
+// lanes of one Lorenz-96 speculative chain when its slots span a whole block
+constexpr int kL96SpecBlockLanes = 256;
+
+
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 

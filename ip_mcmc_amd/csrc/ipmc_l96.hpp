@@ -88,6 +88,7 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
 }
 
 constexpr int kL96Block = 256;
+static_assert(kL96Block == kL96SpecBlockLanes, "block-wide speculation spans one block");
 
 // LDS staging for the in-order misfit / regularizer sums of wide groups
 // (LPC >= 8, group_sumsq); one element otherwise.
@@ -218,9 +219,14 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
   constexpr int M = D / LPC;
   __shared__ T vpark[M][kL96Block];
   __shared__ T stage[l96_stage_len<M, LPC>()];
+  // G == kL96Block: one chain per block, its slots spread over the block's
+  // waves (one per SIMD of the CU, so a round takes the same time), combined
+  // through LDS instead of a wave ballot
+  __shared__ unsigned long long wmask[2][kL96Block / 64];
+  __shared__ T phpark[kL96Block];
   const int t = threadIdx.x;
   const int lane = t & 63;
-  const int G = S * LPC;  // lanes per chain (a power of two <= 64)
+  const int G = S * LPC;  // lanes per chain: a power of two <= 64, or kL96Block
   const int64_t tid = (int64_t)blockIdx.x * kL96Block + t;
   const int64_t chain = tid / G;
   const int r = (int)(tid % G);
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
   for (int j = 0; j < M; ++j) ur[j] = u[j];
   T phu = phi[chain];
   const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
-  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
+  const unsigned long long gmask = (G >= 64) ? ~0ull : ((1ull << G) - 1);
   int nacc = 0, ncalls = 0;
   int64_t st = 0;
   while (st < s.n_steps) {
@@ -266,15 +272,38 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
         acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
       }
     }
-    wave_sync_lds();
     // one bit per slot: the slot's lane sub == 0, at bit slot*LPC
-    const unsigned long long accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
-    const unsigned long long okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
-    const int first = accm ? __builtin_ctzll(accm) / LPC : S;
-    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
-    const int ubits = used * LPC;
-    ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-    const T phf = __shfl(phv, gbase + (first < S ? first : 0) * LPC, 64);
+    int first, used;
+    T phf;
+    if (G <= 64) {
+      wave_sync_lds();
+      const unsigned long long accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
+      const unsigned long long okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
+      first = accm ? __builtin_ctzll(accm) / LPC : S;
+      used = first < S ? first + 1 : (int)(left < S ? left : S);
+      const int ubits = used * LPC;
+      ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+      phf = __shfl(phv, gbase + (first < S ? first : 0) * LPC, 64);
+    } else {
+      const unsigned long long ab = __ballot(acc && sub == 0), ob = __ballot(ok && sub == 0);
+      if (lane == 0) {
+        wmask[0][t >> 6] = ab;
+        wmask[1][t >> 6] = ob;
+      }
+      phpark[t] = phv;
+      __syncthreads();
+      first = S;
+      for (int w = kL96Block / 64 - 1; w >= 0; --w)  // the lowest accepting slot
+        if (wmask[0][w]) first = (w * 64 + __builtin_ctzll(wmask[0][w])) / LPC;
+      used = first < S ? first + 1 : (int)(left < S ? left : S);
+      const int ubits = used * LPC;  // the lanes of the used slots: bits [0, ubits) of the block
+#pragma unroll
+      for (int w = 0; w < kL96Block / 64; ++w) {
+        const int nb = ubits - w * 64;
+        if (nb > 0) ncalls += __builtin_popcountll(wmask[1][w] & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
+      }
+      phf = phpark[(first < S ? first : 0) * LPC];
+    }
     const int win = t - r + (first < S ? first : 0) * LPC + sub;  // the winning slot's lane for my components
     if (s.sum_u && slot == 0) {
       double* su = s.sum_u + chain * D + c0;
@@ -294,7 +323,8 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
       phu = phf;
       ++nacc;
     }
-    wave_sync_lds();  // the parks are rewritten next round
+    if (G <= 64) wave_sync_lds();  // the parks are rewritten next round
+    else __syncthreads();
     st += used;
   }
   if (slot == 0) {

@@ -704,7 +704,7 @@ def test_l96_speculative_sweeps_bit_exact(dev, orc, dtype):
             o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 5, 2**32 - 7, n, dtype, **kw)
             assert 0 < o["acc"].sum() < 21 * n, o["acc"].sum()
             for lanes in lanes_list:
-                for w in (0, 2, 64 // lanes):
+                for w in (0, 2, 64 // lanes, 256 // lanes):  # 256 // lanes: slots over the 4 waves of a block
                     d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 5, 2**32 - 7, n, dtype, dev, lanes=lanes,
                                       cpl=1, spec=w, **kw)
                     _assert_same(d, o, (K, arith, lanes, w, list(kw)))
@@ -714,9 +714,10 @@ def test_l96_speculative_sweeps_bit_exact(dev, orc, dtype):
         rs = np.linspace(0.5, 2.0, K)
         phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
         o = _sweep_oracle(orc, op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, proposal="rw", reg_scale=rs)
-        d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, lanes=lanes_list[-1], cpl=1,
-                          spec=4, proposal="rw", reg_scale=rs)
-        _assert_same(d, o, (K, "rw"))
+        for w in (4, 256 // lanes_list[-1]):
+            d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, lanes=lanes_list[-1], cpl=1,
+                              spec=w, proposal="rw", reg_scale=rs)
+            _assert_same(d, o, (K, "rw", w))
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
