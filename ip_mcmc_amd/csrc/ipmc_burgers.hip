@@ -285,12 +285,15 @@ __device__ T burgers_phi(const ipmc_model& m, const T (&v)[3], const BurCtx& c, 
 constexpr int kBurQMax = 64;
 
 // S speculative slots of GS lanes per chain (S = 1: the sequential chain; S·GS
-// <= 64): slot s evaluates step st+s from the current state as if the steps
-// before it in the round were rejected; the first accepting slot ends the
-// round (see small_spec_kernel) -- bit-identical to S = 1.
+// <= 64, or = kBurBlock: one chain per block, its slots on the block's waves,
+// combined through LDS): slot s evaluates step st+s from the current state as
+// if the steps before it in the round were rejected; the first accepting slot
+// ends the round (see small_spec_kernel) -- bit-identical to S = 1.
 template <typename T, int CPL, int GS, bool FM>
 __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
   __shared__ T lds[kBurBlock * CPL];
+  __shared__ unsigned long long bmask[2][kBurBlock / 64];  // block-wide rounds: the waves' ballots
+  __shared__ T vpk[4][kBurBlock];                          // and every slot's v and Φ(v)
   const int lane = threadIdx.x & 63;
   const int G = S * GS;
   const int64_t tid = (int64_t)blockIdx.x * kBurBlock + threadIdx.x;
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
   const T beta = (T)s.beta, contr = (T)s.contraction;
   T* phi = (T*)s.phi;
   T phu = phi[chain];
-  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
+  const unsigned long long gmask = (G >= 64) ? ~0ull : ((1ull << G) - 1);
   int nacc = 0, ncalls = 0;
   int64_t st = 0;
   while (st < s.n_steps) {
@@ -342,17 +345,46 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
       }
     }
     // one bit per slot (its first lane, bit slot*GS of the chain's lanes)
-    const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
-    const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-    const int first = accm ? __builtin_ctzll(accm) / GS : S;
-    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
-    const int ubits = used * GS;
-    ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-    const int wl = cbase + (first < S ? first : 0) * GS;
-    T vf[3];
+    int first, used;
+    T vf[3], phf;
+    if (G <= 64) {
+      const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
+      const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
+      first = accm ? __builtin_ctzll(accm) / GS : S;
+      used = first < S ? first + 1 : (int)(left < S ? left : S);
+      const int ubits = used * GS;
+      ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+      const int wl = cbase + (first < S ? first : 0) * GS;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
-    const T phf = __shfl(phv, wl, 64);
+      for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
+      phf = __shfl(phv, wl, 64);
+    } else {
+      const int t = threadIdx.x;
+      const unsigned long long ab = __ballot(acc && c.sub == 0), ob = __ballot(ok && c.sub == 0);
+      if (lane == 0) {
+        bmask[0][t >> 6] = ab;
+        bmask[1][t >> 6] = ob;
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) vpk[j][t] = v[j];
+      vpk[3][t] = phv;
+      __syncthreads();
+      first = S;
+      for (int w = kBurBlock / 64 - 1; w >= 0; --w)  // the lowest accepting slot
+        if (bmask[0][w]) first = (w * 64 + __builtin_ctzll(bmask[0][w])) / GS;
+      used = first < S ? first + 1 : (int)(left < S ? left : S);
+      const int ubits = used * GS;
+#pragma unroll
+      for (int w = 0; w < kBurBlock / 64; ++w) {
+        const int nb = ubits - w * 64;
+        if (nb > 0) ncalls += __builtin_popcountll(bmask[1][w] & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
+      }
+      const int wl = (first < S ? first : 0) * GS;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) vf[j] = vpk[j][wl];
+      phf = vpk[3][wl];
+      __syncthreads();  // bmask / vpk are rewritten next round
+    }
     if (s.sum_u && r == 0) {
       for (int q = 0; q < used; ++q) {
 #pragma unroll
@@ -434,11 +466,14 @@ template <int GS>
 static int burgers_spec(const ipmc_sweep& s) {
   if (s.spec_width > 0) {
     const int w = s.spec_width;
-    return ((w & (w - 1)) == 0 && w * GS <= 64) ? w : -1;
+    return ((w & (w - 1)) == 0 && (w * GS <= 64 || w * GS == kBurBlock)) ? w : -1;
   }
   int w = 1;
-  if (s.n_steps > 1)
+  if (s.n_steps > 1) {
     while (w * 2 * GS <= 64 && s.n_chains * (int64_t)GS * w * 2 <= 65536) w *= 2;
+    // a whole block of slots per chain while the ensemble stays within one wave per SIMD
+    if (w * GS == 64 && s.n_chains * (int64_t)kBurBlock <= 65536) w = kBurBlock / GS;
+  }
   return w;
 }
 
@@ -446,7 +481,7 @@ template <typename T, int CPL, int GS, bool FM>
 static int launch_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
   const int S = burgers_spec<GS>(s);
   if (S < 1) {
-    set_error("Burgers: spec_width must be a power of two with spec_width * %d lanes <= 64", GS);
+    set_error("Burgers: spec_width must be a power of two with spec_width * %d lanes <= 64 or = 256", GS);
     return IPMC_ERR_UNSUPPORTED;
   }
   const int64_t blocks = (s.n_chains * GS * S + kBurBlock - 1) / kBurBlock;

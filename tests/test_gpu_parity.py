@@ -735,7 +735,8 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
         cases.append((op, (0, 2, 64 // K)))
     for N, arith in ((128, "reference"), (256, "fma")):
         op = BurgersOperator(N=N, dt_mode="cfl", T=0.2, arith=arith)
-        cases.append((op, (0, 2, 4) if N == 128 else (0, 2)))
+        # the last width spans a whole block (256 lanes: 16 slots of 16 lanes, 8 of 32)
+        cases.append((op, (0, 2, 4, 16) if N == 128 else (0, 2, 8)))
     for op, widths in cases:
         U0, phi0, y, ginv, sq = _problem(op, 19, dtype, orc, seed=3)
         ginv = ginv * 0.2  # broad enough for acceptances inside the rounds
