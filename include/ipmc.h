@@ -122,7 +122,7 @@ typedef struct ipmc_sweep {
                                first acceptance ends the round -- results identical, small ensembles run faster.
                                Lorenz-63 / linear (k <= 8), Lorenz-96 (spec_width * lanes_per_chain <= 64, or = 256:
                                the slots of one chain over the 4 waves of a block),
-                               Burgers (spec_width * lanes of a chain <= 64), two-scale Lorenz-96 (any width
+                               Burgers (spec_width * lanes of a chain <= 64, or = 256), two-scale Lorenz-96 (any width
                                with spec_width * K <= 64). */
   int64_t n_chains;
   int64_t chain_offset;     /* global id of chain 0 of this shard (RNG counter) */
