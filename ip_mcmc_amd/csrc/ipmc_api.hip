@@ -82,6 +82,17 @@ static bool l96_has(int D, int dtype, int lpc, int cpl) {
 //     components per lane: a chain's RK4 step is then a latency chain, and
 //     LDS halos made it 1.6x slower (d=40 at 1 / 64 / 1 024 chains: LPC 4
 //     0.050 / 0.050 / 0.054 ms per step vs LPC 8 0.080 / 0.084 / 0.087).
+// The most lanes per chain whose halos go by DPP (LPC 1, 2, 4, 16) with >= 4
+// components per lane, 0 if none is compiled: the layout of latency-bound
+// chains (small ensembles, speculative slots).
+static int l96_dpp_lpc(int D, int dtype, int cpl) {
+  static const int dpp[4] = {1, 2, 4, 16};
+  int lpc = 0;
+  for (int i = 0; i < 4; ++i)
+    if (D % dpp[i] == 0 && D / dpp[i] >= 4 && l96_has(D, dtype, dpp[i], cpl)) lpc = dpp[i];
+  return lpc;
+}
+
 static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   constexpr int64_t kWaveLanes = 65536;  // 256 CUs x 4 SIMDs x 64 lanes
   static const int dpp[4] = {1, 2, 4, 16};
@@ -115,8 +126,7 @@ static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   lpc = 0;
   for (int ci = ncpl - 1; ci >= 0 && !lpc; --ci) {  // one chain per lane group first
     cpl = cpls[ci];
-    for (int i = 0; i < 4; ++i)
-      if (ok(dpp[i], cpl) && D / dpp[i] >= 4) lpc = dpp[i];
+    lpc = l96_dpp_lpc(D, dtype, cpl);
     for (int i = 0; i < 5 && !lpc; ++i)
       if (ok(all[i], cpl)) lpc = all[i];
   }
@@ -342,10 +352,23 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
       if (spec == 0) {
         spec = 1;
         if (s->n_steps > 1 && s->chains_per_lane != 2) {
-          while (spec * 2 * lpc <= 64 && s->n_chains * (int64_t)lpc * spec * 2 <= 65536) spec *= 2;
+          // speculative slots run on the DPP layout (an LDS-halo layout picked to
+          // fill the GPU with sequential chains is slower than DPP slots: d=40,
+          // 8 192 chains, profiles/r1/small_ensembles.jsonl)
+          int l = lpc;
+          if (!s->lanes_per_chain) {
+            const int d = l96_dpp_lpc(m->dim, s->dtype, 1);
+            if (d) l = d;
+          }
+          int w = 1;
+          while (w * 2 * l <= 64 && s->n_chains * (int64_t)l * w * 2 <= 65536) w *= 2;
           // a whole block of slots per chain (4 waves on the CU's 4 SIMDs) while
           // the ensemble stays within one wave per SIMD
-          if (spec * lpc == 64 && s->n_chains * (int64_t)kL96SpecBlockLanes <= 65536) spec = kL96SpecBlockLanes / lpc;
+          if (w * l == 64 && s->n_chains * (int64_t)kL96SpecBlockLanes <= 65536) w = kL96SpecBlockLanes / l;
+          if (w > 1) {
+            spec = w;
+            lpc = l;
+          }
         }
       }
       if (spec > 1) {
