@@ -42,6 +42,7 @@
  *  - Randomness is counter-based (Philox4x32-10). The draw for (chain, step,
  *    component) is a pure function of (seed, global chain id, global pCN step,
  *    component), so results do not depend on sharding or launch splitting.
+ *    Global chain ids are 32-bit (chain_offset + n_chains <= 2^32, else IPMC_ERR_INVALID).
  */
 #ifndef IPMC_H
 #define IPMC_H
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 5
+#define IPMC_ABI_VERSION 6
 
 typedef enum {
   IPMC_OK = 0,
@@ -125,7 +126,7 @@ typedef struct ipmc_sweep {
                                Burgers (spec_width * lanes of a chain <= 64, or = 256), two-scale Lorenz-96 (any width
                                with spec_width * K <= 64). */
   int64_t n_chains;
-  int64_t chain_offset;     /* global id of chain 0 of this shard (RNG counter) */
+  int64_t chain_offset;     /* global id of chain 0 of this shard (RNG counter); chain_offset + n_chains <= 2^32 */
   void* u;                  /* [n_chains, k] in/out current state */
   void* phi;                /* [n_chains] in/out cached Φ(u) */
   int64_t* accepts;         /* [n_chains] in/out accept counters (may be NULL) */
@@ -148,7 +149,8 @@ typedef struct ipmc_sweep {
   const void* reg_scale;    /* optional [k]: accept on I = Φ + ½Σ(reg_scale_i v_i)² instead of Φ
                                (StandardRWAccepter, accepter.py:98-106); `phi` then caches I(u) */
   uint64_t seed;            /* Philox key */
-  uint64_t step0;           /* global pCN step index of the first step of this launch */
+  uint64_t step0;           /* global pCN step index of the first step of this launch; step0 + n_steps <= 2^63
+                               (steps from 2^63 on are the host-draw range, rng.py) */
   int64_t n_steps;          /* pCN steps in this launch */
   void* sample_out;         /* optional [n_chains, *] : u after the last step, row stride sample_stride elements */
   int64_t sample_stride;
@@ -180,7 +182,7 @@ int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t
                  void* stream);
 
 /* Batched normalised autocorrelation (MCMCSampler.autocorr, sampler.py:43-54):
-   series s is x[s*stride_series + t*stride_t], t < len (len <= 8192);
+   series s is x[s*stride_series + t*stride_t], t < len (any len; series over 8192 samples stream through LDS tiles);
    out[s, tau] = r[tau]/r[0], r[tau] = Σ_t x_[t] x_[t+tau], x_ = x - mean(x), tau < max_lag <= len;
    all ones for a constant series.  out is double [n_series, max_lag]. */
 int ipmc_autocorr(const void* x, int32_t dtype, int64_t n_series, int64_t len, int64_t stride_series,
@@ -195,10 +197,23 @@ int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars,
                  int64_t stride_var, int64_t stride_t, int32_t window, double threshold, uint32_t* flags_scratch,
                  int64_t* out, void* stream);
 
-/* Layout the sweep kernel would use for this model/dtype when lanes_per_chain = chains_per_lane = 0:
-   returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout. */
+/* Lorenz-96 layout of a ONE-step launch (no speculation) when lanes_per_chain = chains_per_lane = 0:
+   returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout.
+   Multi-step launches may speculate on another layout: ipmc_plan_sweep reports that. */
 int ipmc_auto_lanes(const ipmc_model* model, int32_t dtype, int64_t n_chains);
 int ipmc_auto_layout(const ipmc_model* model, int32_t dtype, int64_t n_chains);
+
+/* The kernel plan ipmc_pcn_sweep(model, sweep) would run, from the same code path: lanes per chain
+   (per speculative slot), chains per lane group (2 = packed fp32 pairs) and speculation width
+   (1 = sequential).  Reads only the sweep's dtype, n_chains, n_steps, lanes_per_chain,
+   chains_per_lane and spec_width; returns the error ipmc_pcn_sweep would for an unsupported layout. */
+typedef struct ipmc_plan {
+  int32_t lanes_per_chain;
+  int32_t chains_per_lane;
+  int32_t spec_width;
+  int32_t reserved;
+} ipmc_plan;
+int ipmc_plan_sweep(const ipmc_model* model, const ipmc_sweep* sweep, ipmc_plan* out);
 
 const char* ipmc_last_error(void);
 int ipmc_abi_version(void);

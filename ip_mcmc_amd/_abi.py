@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -85,6 +85,15 @@ class IpmcSweep(C.Structure):
     ]
 
 
+class IpmcPlan(C.Structure):
+    _fields_ = [
+        ("lanes_per_chain", C.c_int32),
+        ("chains_per_lane", C.c_int32),
+        ("spec_width", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
 # Exported symbols of libipmc.so and their ctypes signatures (include/ipmc.h).
 SIGNATURES = {
     "ipmc_pcn_sweep": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.c_void_p]),
@@ -110,6 +119,7 @@ SIGNATURES = {
     ),
     "ipmc_auto_lanes": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_auto_layout": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
+    "ipmc_plan_sweep": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.POINTER(IpmcPlan)]),
     "ipmc_last_error": (C.c_char_p, []),
     "ipmc_abi_version": (C.c_int, []),
 }

@@ -56,7 +56,7 @@ class NpySampleSink:
 class ChainState:
     """Everything needed to continue a run exactly (host numpy arrays)."""
 
-    def __init__(self, u, phi, accepts, calls, seed, step, proposer_i, dtype):
+    def __init__(self, u, phi, accepts, calls, seed, step, proposer_i, dtype, chain_offset=None, accept_kind=None):
         self.u = np.asarray(u)
         self.phi = np.asarray(phi)
         self.accepts = np.asarray(accepts)
@@ -65,6 +65,11 @@ class ChainState:
         self.step = int(step)
         self.proposer_i = int(proposer_i)
         self.dtype = str(dtype)
+        # global id of chain 0 (the Philox streams) and the cached potential's
+        # kind ('pcn': Φ, 'rw_reg': Φ + StandardRWAccepter's regularizer);
+        # None for states written before they were recorded
+        self.chain_offset = None if chain_offset is None else int(chain_offset)
+        self.accept_kind = None if accept_kind is None else str(accept_kind)
 
     @property
     def n_chains(self):
@@ -84,6 +89,8 @@ def save_state(path, state):
         step=np.array(state.step, dtype=np.int64),
         proposer_i=np.array(state.proposer_i, dtype=np.int64),
         dtype=np.array(state.dtype),
+        chain_offset=np.array(-1 if state.chain_offset is None else state.chain_offset, dtype=np.int64),
+        accept_kind=np.array("" if state.accept_kind is None else state.accept_kind),
     )
     return p
 
@@ -91,7 +98,10 @@ def save_state(path, state):
 def load_state(path):
     p = path if path.endswith(".npz") else path + ".npz"
     z = np.load(p, allow_pickle=False)
+    off = int(z["chain_offset"]) if "chain_offset" in z.files else -1
+    kind = str(z["accept_kind"]) if "accept_kind" in z.files else ""
     return ChainState(
         z["u"], z["phi"], z["accepts"], z["calls"] if bool(z["has_calls"]) else None, int(z["seed"]),
-        int(z["step"]), int(z["proposer_i"]), str(z["dtype"]),
+        int(z["step"]), int(z["proposer_i"]), str(z["dtype"]), chain_offset=None if off < 0 else off,
+        accept_kind=kind or None,
     )

@@ -32,6 +32,20 @@ static int fail(int code, const char* msg) {
   return code;
 }
 
+// The Philox counter holds the global chain id in one 32-bit word and the pCN
+// step in two (ipmc_device.hpp); host-side draws (rng.py) use steps from
+// kHostStepBase on.  Ids or steps outside these ranges would alias other
+// chains' draws, so they are rejected.
+constexpr int64_t kChainIdLimit = int64_t(1) << 32;
+constexpr uint64_t kHostStepBase = uint64_t(1) << 63;
+
+static int check_chain_range(int64_t chain_offset, int64_t n_chains) {
+  if (n_chains < 0 || chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (chain_offset > kChainIdLimit - n_chains)
+    return fail(IPMC_ERR_INVALID, "global chain ids (chain_offset + n_chains) must be <= 2^32");
+  return IPMC_OK;
+}
+
 static int check_model(const ipmc_model* m) {
   if (!m) return fail(IPMC_ERR_INVALID, "model is NULL");
   if (m->k <= 0 || m->q <= 0) return fail(IPMC_ERR_INVALID, "model k and q must be positive");
@@ -130,6 +144,55 @@ static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
     for (int i = 0; i < 5 && !lpc; ++i)
       if (ok(all[i], cpl)) lpc = all[i];
   }
+}
+
+// The whole Lorenz-96 sweep plan (layout and speculation width) for a launch:
+// the one place ipmc_pcn_sweep and ipmc_plan_sweep take it from.
+static int l96_plan(const ipmc_model& m, const ipmc_sweep& s, int& lpc, int& cpl, int& spec) {
+  l96_layout(m.dim, s.dtype, s.n_chains, lpc, cpl);
+  if (s.chains_per_lane) cpl = s.chains_per_lane;
+  if (s.lanes_per_chain) lpc = s.lanes_per_chain;
+  if (!lpc || !l96_has(m.dim, s.dtype, lpc, cpl)) {
+    set_error("Lorenz-96: no kernel compiled for dim=%d lanes_per_chain=%d chains_per_lane=%d", m.dim, lpc, cpl);
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  // speculation (l96_spec_kernel): spec_width slots of lpc lanes per chain,
+  // auto = the widest keeping the ensemble within one wave per SIMD
+  spec = s.spec_width;
+  if (spec < 0 || spec > kL96SpecBlockLanes || (spec & (spec - 1)))
+    return fail(IPMC_ERR_UNSUPPORTED, "spec_width must be a power of two <= 256");
+  if (spec == 0) {
+    spec = 1;
+    if (s.n_steps > 1 && s.chains_per_lane != 2) {
+      // speculative slots run on the DPP layout (an LDS-halo layout picked to
+      // fill the GPU with sequential chains is slower than DPP slots: d=40,
+      // 8 192 chains, profiles/r1/small_ensembles.jsonl)
+      int l = lpc;
+      if (!s.lanes_per_chain) {
+        const int d = l96_dpp_lpc(m.dim, s.dtype, 1);
+        if (d) l = d;
+      }
+      int w = 1;
+      while (w * 2 * l <= 64 && s.n_chains * (int64_t)l * w * 2 <= 65536) w *= 2;
+      // a whole block of slots per chain (4 waves on the CU's 4 SIMDs) while
+      // the ensemble stays within one wave per SIMD
+      if (w * l == 64 && s.n_chains * (int64_t)kL96SpecBlockLanes <= 65536) w = kL96SpecBlockLanes / l;
+      if (w > 1) {
+        spec = w;
+        lpc = l;
+      }
+    }
+  }
+  if (spec > 1) {
+    if (spec * lpc > 64 && spec * lpc != kL96SpecBlockLanes)
+      return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: spec_width * lanes_per_chain must be <= 64 or 256");
+    if (cpl == 2) {
+      if (s.chains_per_lane == 2)
+        return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: speculation runs one chain per lane group");
+      cpl = 1;  // the packed fp32 layout is for full ensembles; fp32 one-chain kernels speculate
+    }
+  }
+  return IPMC_OK;
 }
 
 template <typename T, int MODEL, bool FM>
@@ -297,6 +360,39 @@ int ipmc_auto_layout(const ipmc_model* m, int32_t dtype, int64_t n_chains) {
   return 101;
 }
 
+int ipmc_plan_sweep(const ipmc_model* m, const ipmc_sweep* s, ipmc_plan* out) {
+  int rc = check_model(m);
+  if (rc) return rc;
+  if (!s || !out) return fail(IPMC_ERR_INVALID, "sweep / out is NULL");
+  if (s->dtype != IPMC_F32 && s->dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "dtype must be IPMC_F32/F64");
+  int lanes = 1, cpl = 1, spec = 1;
+  switch (m->kind) {
+    case IPMC_MODEL_LINEAR:
+    case IPMC_MODEL_LORENZ63:
+      spec = small_spec_width(*m, *s);
+      if (spec < 0)
+        return fail(IPMC_ERR_UNSUPPORTED, "small models: spec_width must be a power of two <= 64, and 1 for k > 8");
+      break;
+    case IPMC_MODEL_LORENZ96:
+      rc = l96_plan(*m, *s, lanes, cpl, spec);
+      break;
+    case IPMC_MODEL_BURGERS:
+      rc = burgers_plan(*m, *s, lanes, spec);
+      break;
+    case IPMC_MODEL_LORENZ96_2S:
+      rc = l96ts_plan(*m, *s, lanes, spec);
+      break;
+    default:
+      return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
+  }
+  if (rc) return rc;
+  out->lanes_per_chain = lanes;
+  out->chains_per_lane = cpl;
+  out->spec_width = spec;
+  out->reserved = 0;
+  return IPMC_OK;
+}
+
 int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   int rc = check_model(m);
   if (rc) return rc;
@@ -306,8 +402,12 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
     return fail(IPMC_ERR_INVALID, "proposal must be IPMC_PROPOSAL_PCN or IPMC_PROPOSAL_RW");
   if (s->proposal == IPMC_PROPOSAL_PCN && !(s->beta >= 0.0 && s->beta <= 1.0))
     return fail(IPMC_ERR_INVALID, "beta has to be in [0,1]");
-  if (s->n_chains < 0 || s->n_steps < 0 || s->chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (s->n_steps < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  rc = check_chain_range(s->chain_offset, s->n_chains);
+  if (rc) return rc;
   if (s->n_steps > 0x7fffffff) return fail(IPMC_ERR_INVALID, "n_steps per launch must be < 2^31");
+  if (s->step0 > kHostStepBase - (uint64_t)s->n_steps)
+    return fail(IPMC_ERR_INVALID, "pCN steps must stay below 2^63 (the host-draw range)");
   if (s->n_chains == 0 || s->n_steps == 0) {
     if (s->n_chains > 0 && s->sample_out) {
       // no step: the sample is the current state
@@ -336,50 +436,9 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
       return s->dtype == IPMC_F64 ? small_sweep<double>(*m, *s, st) : small_sweep<float>(*m, *s, st);
     }
     case IPMC_MODEL_LORENZ96: {
-      int lpc, cpl;
-      l96_layout(m->dim, s->dtype, s->n_chains, lpc, cpl);
-      if (s->chains_per_lane) cpl = s->chains_per_lane;
-      if (s->lanes_per_chain) lpc = s->lanes_per_chain;
-      if (!lpc || !l96_has(m->dim, s->dtype, lpc, cpl)) {
-        set_error("Lorenz-96: no kernel compiled for dim=%d lanes_per_chain=%d chains_per_lane=%d", m->dim, lpc, cpl);
-        return IPMC_ERR_UNSUPPORTED;
-      }
-      // speculation (l96_spec_kernel): spec_width slots of lpc lanes per chain,
-      // auto = the widest keeping the ensemble within one wave per SIMD
-      int spec = s->spec_width;
-      if (spec < 0 || spec > kL96SpecBlockLanes || (spec & (spec - 1)))
-        return fail(IPMC_ERR_UNSUPPORTED, "spec_width must be a power of two <= 256");
-      if (spec == 0) {
-        spec = 1;
-        if (s->n_steps > 1 && s->chains_per_lane != 2) {
-          // speculative slots run on the DPP layout (an LDS-halo layout picked to
-          // fill the GPU with sequential chains is slower than DPP slots: d=40,
-          // 8 192 chains, profiles/r1/small_ensembles.jsonl)
-          int l = lpc;
-          if (!s->lanes_per_chain) {
-            const int d = l96_dpp_lpc(m->dim, s->dtype, 1);
-            if (d) l = d;
-          }
-          int w = 1;
-          while (w * 2 * l <= 64 && s->n_chains * (int64_t)l * w * 2 <= 65536) w *= 2;
-          // a whole block of slots per chain (4 waves on the CU's 4 SIMDs) while
-          // the ensemble stays within one wave per SIMD
-          if (w * l == 64 && s->n_chains * (int64_t)kL96SpecBlockLanes <= 65536) w = kL96SpecBlockLanes / l;
-          if (w > 1) {
-            spec = w;
-            lpc = l;
-          }
-        }
-      }
-      if (spec > 1) {
-        if (spec * lpc > 64 && spec * lpc != kL96SpecBlockLanes)
-          return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: spec_width * lanes_per_chain must be <= 64 or 256");
-        if (cpl == 2) {
-          if (s->chains_per_lane == 2)
-            return fail(IPMC_ERR_UNSUPPORTED, "Lorenz-96: speculation runs one chain per lane group");
-          cpl = 1;  // the packed fp32 layout is for full ensembles; fp32 one-chain kernels speculate
-        }
-      }
+      int lpc, cpl, spec;
+      rc = l96_plan(*m, *s, lpc, cpl, spec);
+      if (rc) return rc;
       return s->dtype == IPMC_F64 ? l96_sweep_f64(*m, *s, lpc, spec, st)
                                   : l96_sweep_f32(*m, *s, lpc, cpl, spec, st);
     }
@@ -427,7 +486,9 @@ int ipmc_forward(const ipmc_model* m, int32_t dtype, int64_t n, const void* u, v
 
 int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, int32_t k, int32_t dtype,
                 void* out, void* stream) {
-  if (n_chains < 0 || k < 0 || chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (k < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  const int rc = check_chain_range(chain_offset, n_chains);
+  if (rc) return rc;
   if (dtype != IPMC_F32 && dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "bad dtype");
   const int64_t total = n_chains * k;
   if (total == 0) return IPMC_OK;
@@ -443,7 +504,8 @@ int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t 
 }
 
 int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out, void* stream) {
-  if (n_chains < 0 || chain_offset < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  const int rc = check_chain_range(chain_offset, n_chains);
+  if (rc) return rc;
   if (n_chains == 0) return IPMC_OK;
   if (!out) return fail(IPMC_ERR_INVALID, "out is NULL");
   const int64_t blocks = (n_chains + 255) / 256;

@@ -558,6 +558,19 @@ int burgers_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
   return fm ? dispatch<float, true>(cpl, gs, l) : dispatch<float, false>(cpl, gs, l);
 }
 
+int burgers_plan(const ipmc_model& m, const ipmc_sweep& s, int& lanes, int& spec) {
+  int cpl, gs;
+  const int rc = validate(m, s.n_chains, s.lanes_per_chain, cpl, gs);
+  if (rc) return rc;
+  lanes = gs;
+  spec = gs == 16 ? burgers_spec<16>(s) : gs == 32 ? burgers_spec<32>(s) : burgers_spec<64>(s);
+  if (spec < 1) {
+    set_error("Burgers: spec_width must be a power of two with spec_width * %d lanes <= 64 or = 256", gs);
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  return IPMC_OK;
+}
+
 int burgers_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
                  void* out, bool phi, hipStream_t st) {
   int cpl, gs;

@@ -9,7 +9,9 @@
 //
 // One workgroup per series: the series is staged once in LDS (coalesced
 // strided load), the mean is a block reduction, and each thread owns lags
-// tau = tid, tid + 256, ... with the inner sum over t read from LDS.
+// tau = tid, tid + 256, ... with the inner sum over t read from LDS.  Longer
+// series (> kAcMaxLen samples) stream through LDS tiles instead
+// (autocorr_long_kernel), with the same summation order.
 #include "ipmc_internal.hpp"
 
 namespace ipmc {
@@ -62,6 +64,80 @@ __global__ __launch_bounds__(kAcBlock) void autocorr_kernel(const T* __restrict_
     for (int64_t t = 0; t + tau < len; ++t) r += xs[t] * xs[t + tau];
     o[tau] = r / r0;
   }
+}
+
+// Series longer than kAcMaxLen: the same sums from global memory.  A block
+// owns kAcBlock consecutive lags of one series (grid: series x lag tiles),
+// recomputes the mean and r[0] with the short kernel's strided-partials + tree
+// order, and streams the series through LDS in tiles of kAcTile samples:
+// a = x_[t0 .. t0+kAcTile), b = x_[t0+tau0 .. t0+tau0+kAcTile+kAcBlock).
+// Each thread's r[tau] is still the ascending sum over t, so the results equal
+// the short kernel's bit for bit.
+constexpr int kAcTile = 2048;
+
+template <typename T>
+__device__ double ac_block_sum(const T* src, int64_t len, int64_t stride_t, double sub, bool square, double* red) {
+  double part = 0.0;
+  for (int64_t t = threadIdx.x; t < len; t += kAcBlock) {
+    const double v = (double)src[t * stride_t];
+    if (square) {
+      const double c = v - sub;
+      part += c * c;
+    } else {
+      part += v;
+    }
+  }
+  red[threadIdx.x] = part;
+  __syncthreads();
+  for (int off = kAcBlock / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kAcBlock) void autocorr_long_kernel(const T* __restrict__ x, int64_t n_series,
+                                                                  int64_t len, int64_t stride_series,
+                                                                  int64_t stride_t, int max_lag,
+                                                                  double* __restrict__ out) {
+  __shared__ double a[kAcTile];
+  __shared__ double b[kAcTile + kAcBlock];
+  __shared__ double red[kAcBlock];
+  const int64_t s = blockIdx.x;
+  const int tau0 = blockIdx.y * kAcBlock;
+  if (s >= n_series || tau0 >= max_lag) return;
+  const T* src = x + s * stride_series;
+  const double mean = ac_block_sum(src, len, stride_t, 0.0, false, red) / (double)len;
+  const double r0 = ac_block_sum(src, len, stride_t, mean, true, red);
+  const int tau = tau0 + (int)threadIdx.x;
+  double* o = out + s * max_lag;
+  if (r0 == 0.0) {
+    if (tau < max_lag) o[tau] = 1.0;
+    return;
+  }
+  double r = 0.0;
+  for (int64_t t0 = 0; t0 + tau0 < len; t0 += kAcTile) {
+    for (int i = threadIdx.x; i < kAcTile; i += kAcBlock) {
+      const int64_t t = t0 + i;
+      a[i] = t < len ? (double)src[t * stride_t] - mean : 0.0;
+    }
+    for (int i = threadIdx.x; i < kAcTile + kAcBlock; i += kAcBlock) {
+      const int64_t t = t0 + tau0 + i;
+      b[i] = t < len ? (double)src[t * stride_t] - mean : 0.0;
+    }
+    __syncthreads();
+    if (tau < max_lag) {
+      const int64_t rem = len - tau - t0;  // terms t0 + i with t0 + i + tau < len
+      const int n = rem < kAcTile ? (int)(rem > 0 ? rem : 0) : kAcTile;
+      const int sh = (int)threadIdx.x;
+      for (int i = 0; i < n; ++i) r += a[i] * b[i + sh];
+    }
+    __syncthreads();
+  }
+  if (tau < max_lag) o[tau] = r / r0;
 }
 
 // ---------------------------------------------------------------- burn-in
@@ -239,15 +315,29 @@ extern "C" int ipmc_autocorr(const void* x, int32_t dtype, int64_t n_series, int
     set_error("ipmc_autocorr: empty series or NULL pointer");
     return IPMC_ERR_INVALID;
   }
-  if (len > kAcMaxLen) {
-    set_error("ipmc_autocorr: series longer than %d samples (split into windows)", kAcMaxLen);
-    return IPMC_ERR_UNSUPPORTED;
-  }
   if (max_lag > len) {
     set_error("ipmc_autocorr: max_lag %d exceeds the series length %lld", max_lag, (long long)len);
     return IPMC_ERR_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (len > kAcMaxLen) {
+    if (n_series > 0x7fffffff) {
+      set_error("ipmc_autocorr: at most 2^31 - 1 long series per call");
+      return IPMC_ERR_INVALID;
+    }
+    const dim3 grid((unsigned)n_series, (unsigned)((max_lag + kAcBlock - 1) / kAcBlock));
+    if (dtype == IPMC_F64)
+      hipLaunchKernelGGL(autocorr_long_kernel<double>, grid, dim3(kAcBlock), 0, st, (const double*)x, n_series, len,
+                         stride_series, stride_t, max_lag, out);
+    else if (dtype == IPMC_F32)
+      hipLaunchKernelGGL(autocorr_long_kernel<float>, grid, dim3(kAcBlock), 0, st, (const float*)x, n_series, len,
+                         stride_series, stride_t, max_lag, out);
+    else {
+      set_error("ipmc_autocorr: bad dtype");
+      return IPMC_ERR_INVALID;
+    }
+    return check_launch("autocorr_long_kernel");
+  }
   if (dtype == IPMC_F64)
     hipLaunchKernelGGL(autocorr_kernel<double>, dim3((unsigned)n_series), dim3(kAcBlock), 0, st, (const double*)x,
                        n_series, len, stride_series, stride_t, max_lag, out);

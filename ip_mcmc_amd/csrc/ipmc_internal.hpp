@@ -28,11 +28,14 @@ bool l96_has_f64(int D, int lpc);
 
 // Burgers (ipmc_burgers.hip)
 int burgers_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st);
+// lanes per chain and speculation width burgers_sweep would use
+int burgers_plan(const ipmc_model& m, const ipmc_sweep& s, int& lanes, int& spec);
 int burgers_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
                  void* out, bool phi, hipStream_t st);
 
 // Two-scale Lorenz-96 with the moment observation (ipmc_l96ts.hip)
 int l96ts_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st);
+int l96ts_plan(const ipmc_model& m, const ipmc_sweep& s, int& lanes, int& spec);
 int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
                void* out, bool phi, hipStream_t st);
 

@@ -18,6 +18,12 @@ constexpr bool l96_ok() {
   return LPC <= 16 && D % LPC == 0 && D / LPC >= 2 && (D / LPC) * (int)sizeof(T) <= 160;
 }
 
+// An (D, LPC) pair with no instantiation: report it through ipmc_last_error.
+inline int l96_unsupported(const ipmc_model& m, int lpc, const char* what) {
+  set_error("Lorenz-96: no %s kernel compiled for dim=%d lanes_per_chain=%d", what, m.dim, lpc);
+  return IPMC_ERR_UNSUPPORTED;
+}
+
 // spec > 1: the speculative kernel with spec slots of LPC lanes per chain.
 template <typename T, int D, int LPC, bool FM>
 int l96_launch_sweep(const ipmc_model& m, const ipmc_sweep& s, int spec, hipStream_t st) {
@@ -57,7 +63,7 @@ int l96_sweep_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hip
     IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
 #undef IPMC_CASE
   }
-  return IPMC_ERR_UNSUPPORTED;
+  return l96_unsupported(m, lpc, "sweep");
 }
 
 template <int D, int LPC, bool FM>
@@ -79,7 +85,7 @@ int l96_sweep_pk_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_
     IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
 #undef IPMC_CASE
   }
-  return IPMC_ERR_UNSUPPORTED;
+  return l96_unsupported(m, lpc, "packed fp32 sweep");
 }
 
 inline int l96_sweep_pk(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
@@ -90,7 +96,7 @@ inline int l96_sweep_pk(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipSt
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }
-  return IPMC_ERR_UNSUPPORTED;
+  return l96_unsupported(m, lpc, "dimension's");
 }
 
 template <typename T, int D, bool FM>
@@ -104,7 +110,7 @@ int l96_eval_d(const ipmc_model& m, int64_t n, const void* u, const void* y, con
     IPMC_CASE(1) IPMC_CASE(2) IPMC_CASE(4) IPMC_CASE(8) IPMC_CASE(16)
 #undef IPMC_CASE
   }
-  return IPMC_ERR_UNSUPPORTED;
+  return l96_unsupported(m, lpc, "evaluation");
 }
 
 template <typename T>
@@ -117,7 +123,7 @@ int l96_sweep_t(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hip
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }
-  return IPMC_ERR_UNSUPPORTED;
+  return l96_unsupported(m, lpc, "dimension's");
 }
 
 template <typename T>
@@ -132,7 +138,7 @@ int l96_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* y, con
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }
-  return IPMC_ERR_UNSUPPORTED;
+  return l96_unsupported(m, lpc, "dimension's");
 }
 
 template <typename T, int D>

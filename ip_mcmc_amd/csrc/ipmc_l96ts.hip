@@ -492,6 +492,25 @@ int l96ts_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
   return fm ? ts_sweep_t<float, true, 1>(m, s, st) : ts_sweep_t<float, false, 1>(m, s, st);
 }
 
+int l96ts_plan(const ipmc_model& m, const ipmc_sweep& s, int& lanes, int& spec) {
+  if (m.dim > 64) {
+    set_error("two-scale Lorenz-96: K <= 64");
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  const int spl = ts_spl(m, &s);
+  if (spl < 0) {
+    set_error("two-scale Lorenz-96: lanes_per_chain must be K or (K even, J <= 10) K/2");
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  lanes = m.dim / spl;
+  spec = ts_spec(s, lanes);
+  if (spec < 1) {
+    set_error("two-scale Lorenz-96: spec_width * lanes per chain (%d) must be <= 64", lanes);
+    return IPMC_ERR_UNSUPPORTED;
+  }
+  return IPMC_OK;
+}
+
 int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, const void* y, const void* ginv,
                void* out, bool phi, hipStream_t st) {
   if (m.dim > 64) {

@@ -13,14 +13,18 @@ concurrent chains, so the device draws are a pure function of
 
 ``PhiloxRNG`` is the user-facing handle: the sampler reads ``seed`` and
 ``step`` and advances ``step`` by the pCN steps it ran, so two successive
-``run`` calls continue one stream exactly as a Generator would.
+``run`` calls continue one stream exactly as a Generator would (an int seed or
+numpy Generator given to the sampler is resolved into one PhiloxRNG once, on
+the first run, and kept).
 """
 import numpy as np
 
 _MASK64 = (1 << 64) - 1
-# Host-side draws (GaussianDistribution.sample with a PhiloxRNG) use chain ids
-# from this offset on, away from any sampler chain.
-HOST_CHAIN_BASE = 1 << 31
+# Host-side draws (GaussianDistribution.sample with a PhiloxRNG) use pCN steps
+# from this offset on (chain id 0), away from any sampler step: the C-ABI
+# rejects sweeps that would reach it, and sampler chain ids may use the whole
+# 32-bit counter word (include/ipmc.h).
+HOST_STEP_BASE = 1 << 63
 
 
 class PhiloxRNG:
@@ -50,7 +54,7 @@ class PhiloxRNG:
 
     def host_normals(self, k):
         """k fresh standard normals as a numpy array (drawn on the device)."""
-        z = self.normals(1, k, step=0, chain_offset=HOST_CHAIN_BASE + self._host_draws)
+        z = self.normals(1, k, step=HOST_STEP_BASE + self._host_draws, chain_offset=0)
         self._host_draws += 1
         return z.double().cpu().numpy().reshape(k)
 

@@ -178,13 +178,17 @@ class MCMCSampler:
         if n_samples < 0 or sample_interval < 0:
             raise ValueError("n_samples and sample_interval must be >= 0")
 
+        # the seed is resolved once and kept, so the Philox position carries
+        # over between runs like the reference's one Generator (code.org:12-13)
+        if not isinstance(self.rng, PhiloxRNG):
+            self.rng = resolve_rng(self.rng)
+        rng = self.rng
+        accept_kind = "rw_reg" if plan.reg_scale is not None else "pcn"
         if resume:
-            rng = self.rng if isinstance(self.rng, PhiloxRNG) else PhiloxRNG()
+            _check_resume(u_0, self.chain_offset, accept_kind)
             rng.seed, rng.step = u_0.seed, u_0.step
             if hasattr(plan.proposer, "i"):
                 plan.proposer.i = u_0.proposer_i
-        else:
-            rng = resolve_rng(self.rng)
         if isinstance(self.accepter, CountedAccepter):
             self.accepter.reset()  # sampler.py:15-16
 
@@ -227,11 +231,14 @@ class MCMCSampler:
             sw.beta, sw.contraction = plan.proposer.device_step()
         sw.seed = rng.seed
         # the accept potential of the starting states: Φ(u), or I(u) for StandardRWAccepter
-        if resume:
-            if u_0.phi.shape[0] != n_chains:
-                raise ValueError("ChainState phi does not match its u")
+        state_dtype = "float64" if td == torch.float64 else "float32"
+        if resume and u_0.phi.shape[0] != n_chains:
+            raise ValueError("ChainState phi does not match its u")
+        if resume and u_0.dtype == state_dtype:
             phi.copy_(dev.to_device(u_0.phi, td, device))
         else:
+            # a fresh run, or a state saved in the other precision: its Φ cache
+            # is not this dtype's Φ(u), so recompute it
             call("ipmc_init_phi", C.byref(model), C.byref(sw), stream)
 
         step = rng.step
@@ -331,8 +338,8 @@ class MCMCSampler:
         prev_calls = u_0.calls if (resume and u_0.calls is not None) else 0
         self.state = ChainState(
             U.cpu().numpy(), phi.cpu().numpy(), prev_acc + acc_np,
-            None if calls_np is None else prev_calls + calls_np, rng.seed, rng.step, prop_i,
-            "float64" if td == torch.float64 else "float32",
+            None if calls_np is None else prev_calls + calls_np, rng.seed, rng.step, prop_i, state_dtype,
+            chain_offset=self.chain_offset, accept_kind=accept_kind,
         )
         self.state.steps_this_run = total
         if keep == "samples":
@@ -372,6 +379,23 @@ class MCMCSampler:
         from .diagnostics import autocorr
 
         return autocorr(np.asarray(x, dtype=np.float64).reshape(-1))
+
+
+def _check_resume(state, chain_offset, accept_kind):
+    """A ChainState continues exactly only on the same Philox streams (global
+    chain ids) and the same accept potential (Φ for pCNAccepter, I = Φ + the
+    regularizer for StandardRWAccepter); anything else is an error.  States
+    saved before these fields existed carry None and are not checked."""
+    if state.chain_offset is not None and state.chain_offset != chain_offset:
+        raise ValueError(
+            f"ChainState was saved with chain_offset={state.chain_offset}, the sampler has {chain_offset}: "
+            "the chains would continue on other Philox streams"
+        )
+    if state.accept_kind is not None and state.accept_kind != accept_kind:
+        raise ValueError(
+            f"ChainState caches the {state.accept_kind!r} accept potential, this sampler accepts on "
+            f"{accept_kind!r} (pcn = pCNAccepter's Φ, rw_reg = StandardRWAccepter's Φ + regularizer)"
+        )
 
 
 # page-locked host buffers up to this size; larger sample arrays use pageable

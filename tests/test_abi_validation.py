@@ -148,8 +148,8 @@ def test_eval_and_rng_checks(h):
 def test_diagnostics_checks(h):
     _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, 1, 10, 10, 1, 11, DUMMY, None), _abi.ERR_INVALID,
             "exceeds the series length")
-    _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, 1, 9000, 9000, 1, 10, DUMMY, None), _abi.ERR_UNSUPPORTED,
-            "longer than 8192")
+    _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, 1, 9000, 9000, 1, 9001, DUMMY, None), _abi.ERR_INVALID,
+            "exceeds the series length")  # the long-series path checks the same way
     _status(h, h.ipmc_autocorr(DUMMY, _abi.F64, -1, 10, 10, 1, 5, DUMMY, None), _abi.ERR_INVALID, "negative")
     assert h.ipmc_autocorr(None, _abi.F64, 0, 10, 10, 1, 5, None, None) == _abi.OK
     _status(h, h.ipmc_burn_in(DUMMY, _abi.F64, 2, 3, 49, 147, 49, 1, 50, 0.03, DUMMY, DUMMY, None),
@@ -199,3 +199,88 @@ def test_python_layer_raises_with_the_library_message():
         s = _sweep()
         s.beta = 2.0
         call("ipmc_pcn_sweep", C.byref(_model()), C.byref(s), None)
+
+
+def test_chain_id_and_step_ranges(h):
+    """Global chain ids live in one 32-bit Philox counter word and pCN steps
+    below 2^63 (the host-draw range starts there): anything outside would alias
+    other chains' draws, so the ABI rejects it before launching."""
+    m = C.byref(_model())
+    s = _sweep()
+    s.chain_offset = (1 << 32) - 4  # 8 chains -> ids up to 2^32 + 3
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "<= 2^32")
+    s = _sweep()
+    s.step0 = (1 << 63) - 1
+    s.n_steps = 2
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "below 2^63")
+    _status(h, h.ipmc_normal(1, (1 << 32) - 1, 2, 0, 4, _abi.F64, DUMMY, None), _abi.ERR_INVALID, "<= 2^32")
+    _status(h, h.ipmc_uniform(1, 1 << 32, 1, 0, DUMMY, None), _abi.ERR_INVALID, "<= 2^32")
+    _status(h, h.ipmc_uniform(1, -1, 1, 0, DUMMY, None), _abi.ERR_INVALID, "negative")
+    # the last valid id is fine for validation (n = 0 -> no launch)
+    assert h.ipmc_uniform(1, 1 << 32, 0, 0, DUMMY, None) == _abi.OK
+
+
+def _plan(h, model, sweep):
+    p = _abi.IpmcPlan()
+    rc = h.ipmc_plan_sweep(C.byref(model), C.byref(sweep), C.byref(p))
+    assert rc == _abi.OK, h.ipmc_last_error()
+    return p.lanes_per_chain, p.chains_per_lane, p.spec_width
+
+
+def test_plan_sweep_reports_what_the_sweep_runs(h):
+    """ipmc_plan_sweep comes from the same code path as ipmc_pcn_sweep's kernel
+    choice, including the speculation of multi-step launches (which may run on
+    another layout than ipmc_auto_layout's one-step pick)."""
+    m = _model(dim=40, k=40, q=40)
+    s = _sweep(n=65536)
+    assert _plan(h, m, s) == (4, 1, 1)  # headline: 4 lanes per chain, sequential
+    s.dtype = _abi.F32
+    assert _plan(h, m, s) == (4, 2, 1)  # packed fp32 pairs
+    s = _sweep(n=8192)
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 8192) == 108  # one step: LDS halos fill the GPU
+    assert _plan(h, m, s) == (8, 1, 1)
+    s.n_steps = 16
+    assert _plan(h, m, s) == (4, 1, 2)  # multi-step: DPP layout with 2 speculative slots
+    s = _sweep(n=1)
+    s.n_steps = 16
+    assert _plan(h, m, s) == (4, 1, 64)  # one chain: its slots span a whole block
+    s.spec_width = 1
+    assert _plan(h, m, s) == (4, 1, 1)
+    s.spec_width = 3
+    rc = h.ipmc_plan_sweep(C.byref(m), C.byref(s), C.byref(_abi.IpmcPlan()))
+    _status(h, rc, _abi.ERR_UNSUPPORTED, "power of two")
+    # small models: one lane per slot
+    ml = _model(kind=_abi.MODEL_LORENZ63, k=3, q=6, dim=3)
+    s = _sweep(n=4096)
+    s.n_steps = 128
+    assert _plan(h, ml, s) == (1, 1, 16)  # cfg 2: width 16 (profiles/r1/spec_cfg2.txt)
+    # two-scale: K lanes per chain (K=36: 2 slow variables per lane)
+    mt = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=30, dim=6)
+    mt.fast_per_slow = 4
+    s = _sweep(n=65536)
+    assert _plan(h, mt, s) == (6, 1, 1)
+    mt = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=180, dim=36)
+    mt.fast_per_slow = 10
+    assert _plan(h, mt, s)[0] == 18
+    # Burgers N=256: 32 lanes of 8 cells
+    mb = _model(kind=_abi.MODEL_BURGERS, k=3, q=5, dim=256)
+    mb.n_windows = 5
+    mb.win_lo = mb.win_hi = DUMMY
+    s = _sweep(n=2048)
+    assert _plan(h, mb, s) == (32, 1, 1)
+    s = _sweep(n=1)
+    s.n_steps = 8
+    assert _plan(h, mb, s) == (32, 1, 8)
+    rc = h.ipmc_plan_sweep(None, C.byref(s), C.byref(_abi.IpmcPlan()))
+    _status(h, rc, _abi.ERR_INVALID, "model is NULL")
+
+
+def test_unsupported_layout_sets_the_error_message(h):
+    """A forced layout with no compiled kernel reports why (not a stale message)."""
+    m = C.byref(_model(dim=40, k=40, q=40))
+    s = _sweep()
+    s.beta = 2.0
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "beta")  # leave a message behind
+    s = _sweep()
+    s.lanes_per_chain = 3
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_UNSUPPORTED, "lanes_per_chain=3")

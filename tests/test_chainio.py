@@ -43,6 +43,27 @@ def test_state_roundtrip(tmp_path):
     r = load_state(p)
     assert r.seed == st.seed and r.step == 12345 and r.proposer_i == 77 and r.dtype == "float32"
     assert np.array_equal(r.u, st.u) and np.array_equal(r.phi, st.phi) and r.calls is None
+    assert r.chain_offset is None and r.accept_kind is None  # not recorded -> not checked on resume
+    st = ChainState(np.ones((4, 3)), np.arange(4.0), np.arange(4), np.arange(4), 7, 8, 0, "float64",
+                    chain_offset=4096, accept_kind="rw_reg")
+    r = load_state(save_state(str(tmp_path / "st2"), st))
+    assert r.chain_offset == 4096 and r.accept_kind == "rw_reg" and np.array_equal(r.calls, np.arange(4))
+
+
+def test_resume_rejects_other_streams_or_potential():
+    """A state continues exactly only on its own Philox streams (chain_offset)
+    and accept potential (pCN's Φ vs StandardRWAccepter's Φ + regularizer)."""
+    from ip_mcmc_amd.chainio import ChainState
+    from ip_mcmc_amd.sampler import _check_resume
+
+    st = ChainState(np.ones((2, 3)), np.zeros(2), np.zeros(2), None, 1, 10, 0, "float64", chain_offset=64,
+                    accept_kind="pcn")
+    _check_resume(st, 64, "pcn")
+    with pytest.raises(ValueError, match="chain_offset=64"):
+        _check_resume(st, 0, "pcn")
+    with pytest.raises(ValueError, match="accept potential"):
+        _check_resume(st, 64, "rw_reg")
+    _check_resume(ChainState(np.ones((2, 3)), np.zeros(2), np.zeros(2), None, 1, 10, 0, "float64"), 5, "rw_reg")
 
 
 @pytest.mark.gpu
@@ -70,3 +91,54 @@ def test_resume_is_exact_and_streaming_matches(tmp_path):
         assert np.array_equal(np.concatenate([a, np.asarray(b)], axis=1), full)
         assert np.array_equal(s2.checkpoint().u, s_full.checkpoint().u)
         assert np.array_equal(s2.checkpoint().accepts, s_full.checkpoint().accepts)
+
+
+@pytest.mark.gpu
+def test_back_to_back_runs_continue_one_stream():
+    """Two run() calls on one sampler with an int seed (or a numpy Generator)
+    equal one run of the same total length: the seed is resolved once and the
+    Philox position carries over, as the reference's one Generator does; the
+    variable-step proposer's counter and its noise stay in step."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             Lorenz96Operator, MCMCSampler, VarSteppCNProposer, pCNAccepter)
+
+    op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=40)
+    y = op(np.zeros(8)) + 0.05
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(8), 0.01 * np.eye(8)))
+    prior = GaussianDistribution(np.zeros(8), np.eye(8))
+    for make in (lambda: ConstSteppCNProposer(0.3, prior), lambda: VarSteppCNProposer(lambda i: 0.1 + 0.2 / i, prior)):
+        for seed in (11, lambda: np.random.default_rng(4)):
+            rng = (lambda: seed) if isinstance(seed, int) else seed
+            u0 = np.zeros((17, 8))
+            full = MCMCSampler(make(), CountedAccepter(pCNAccepter(pot)), rng()).run(
+                u0, n_samples=9, burn_in=20, sample_interval=4)
+            acc = CountedAccepter(pCNAccepter(pot))
+            s = MCMCSampler(make(), acc, rng())
+            a = s.run(u0, n_samples=5, burn_in=20, sample_interval=4)
+            b = s.run(a[:, -1], n_samples=4, burn_in=4, sample_interval=4)  # burn-in max(0, 4 - 4) = 0
+            assert np.array_equal(np.concatenate([a, b], axis=1), full)
+            assert np.all(np.asarray(acc.calls) == 16)  # CountedAccepter.reset() per run (sampler.py:15-16)
+
+
+@pytest.mark.gpu
+def test_resume_checks_offset_and_recomputes_phi_across_dtypes():
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, Lorenz96Operator,
+                             MCMCSampler, PhiloxRNG, pCNAccepter)
+
+    op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=40)
+    y = op(np.zeros(8)) + 0.05
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(8), 0.01 * np.eye(8)))
+    prop = ConstSteppCNProposer(0.3, GaussianDistribution(np.zeros(8), np.eye(8)))
+    s = MCMCSampler(prop, pCNAccepter(pot), 3, chain_offset=128)
+    s.run(np.zeros((6, 8)), n_samples=2, burn_in=4, sample_interval=2)
+    st = s.checkpoint()
+    assert st.chain_offset == 128 and st.accept_kind == "pcn"
+    with pytest.raises(ValueError, match="chain_offset"):
+        MCMCSampler(prop, pCNAccepter(pot), 3).run(st, n_samples=1, burn_in=0, sample_interval=2)
+    # an f64 state continued in f32: Φ is recomputed in f32, equal to a fresh f32 run from the same u
+    f32 = MCMCSampler(prop, pCNAccepter(pot), 3, chain_offset=128, dtype=np.float32)
+    f32.run(st, n_samples=1, burn_in=0, sample_interval=2)
+    ref = MCMCSampler(prop, pCNAccepter(pot), PhiloxRNG(3, st.step), chain_offset=128, dtype=np.float32)
+    ref.run(st.u, n_samples=1, burn_in=2, sample_interval=2)  # max(0, 2 - 2) + 1 * 2 steps
+    assert np.array_equal(f32.checkpoint().u, ref.checkpoint().u)
+    assert np.array_equal(f32.checkpoint().phi, ref.checkpoint().phi)

@@ -33,6 +33,30 @@ def test_autocorr_lags_and_dtypes(orc):
     np.testing.assert_allclose(got32, ref, rtol=0, atol=2e-5)
 
 
+def test_autocorr_of_series_longer_than_lds(orc):
+    """Series over 8 192 samples (MCMCSampler.autocorr on a whole long chain,
+    sampler.py:43-54 accepts any length) go through the LDS-tiled kernel:
+    all lags of a 12 000-sample chain, partial lags of a batch, a constant
+    series (ones), f32 input, and a strided (C, n, k) chain layout."""
+    from ip_mcmc_amd import MCMCSampler
+    from ip_mcmc_amd.diagnostics import autocorr, chain_autocorr
+
+    rng = np.random.default_rng(11)
+    x = rng.normal(size=12000).cumsum()
+    np.testing.assert_allclose(MCMCSampler.autocorr(x), orc.autocorr_ref(x), rtol=1e-10, atol=1e-12)
+    b = rng.normal(size=(3, 9001)).cumsum(axis=-1)
+    b[1] = 2.5
+    got = autocorr(b, max_lag=700)
+    assert got.shape == (3, 700) and np.all(got[1] == 1.0)
+    for i in (0, 2):
+        np.testing.assert_allclose(got[i], orc.autocorr_ref(b[i])[:700], rtol=1e-10, atol=1e-12)
+    got32 = autocorr(torch.as_tensor(b, dtype=torch.float32).cuda(), max_lag=300).cpu().numpy()
+    np.testing.assert_allclose(got32[0], orc.autocorr_ref(b[0].astype(np.float32))[:300], rtol=0, atol=2e-5)
+    samples = rng.normal(size=(2, 10000, 3)).cumsum(axis=1)
+    got = chain_autocorr(samples, 257)
+    np.testing.assert_allclose(got[1, 2], orc.autocorr_ref(samples[1, :, 2])[:257], rtol=1e-10, atol=1e-12)
+
+
 def test_autocorrelation_windows_and_chain_layout(orc):
     """helpers.autocorrelation (helpers.py:41-54) restated with the reference's
     per-window MCMCSampler.autocorr (the oracle's restatement), and the (C, n, k) chain layout."""
