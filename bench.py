@@ -75,19 +75,20 @@ class Workload:
         s.beta, s.contraction = BETA, float(np.sqrt(1 - BETA**2))
         s.seed, s.step0, s.n_steps = 2, 0, 1
         self.s = s
-        auto = call_auto(self.model, adt, n_chains)
-        self.lanes = auto % 100 if lanes == 0 else lanes
-        self.chains_per_lane = auto // 100 if chains_per_lane == 0 else chains_per_lane
+        # the plan the sweep runs (ipmc_plan_sweep: same code path as the launch)
+        self.lanes, self.chains_per_lane, self.spec_width = sweep_plan(self.model, s)
 
     def step(self):
         call("ipmc_pcn_sweep", C.byref(self.model), C.byref(self.s), self.stream)
         self.s.step0 += 1
 
 
-def call_auto(model, adt, n):
-    from ip_mcmc_amd._lib import lib
-
-    return lib().ipmc_auto_layout(C.byref(model), adt, n)
+def sweep_plan(model, sweep):
+    """(lanes per chain, chains per lane group, speculation width) of the kernel
+    ipmc_pcn_sweep runs for this model and sweep."""
+    p = _abi.IpmcPlan()
+    call("ipmc_plan_sweep", C.byref(model), C.byref(sweep), C.byref(p))
+    return p.lanes_per_chain, p.chains_per_lane, p.spec_width
 
 
 def pmc_traffic(dtype, chains):
@@ -284,6 +285,7 @@ def main():
                 "arith": "fma",
                 "lanes_per_chain": w.lanes,
                 "chains_per_lane": w.chains_per_lane,
+                "spec_width": w.spec_width,
                 "parallelism": f"chains sharded over {world} GPU(s)",
             },
             "roofline": {

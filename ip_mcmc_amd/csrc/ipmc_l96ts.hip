@@ -21,6 +21,9 @@ constexpr int kTsBlock = 256;
 // 1 + J values per lane plus the chain state.
 template <typename T, int J, int SPL>
 constexpr int ts_waves() {
+#ifdef IPMC_TS_WAVES  // layout experiments (tools/)
+  return IPMC_TS_WAVES;
+#endif
   if constexpr (SPL == 2) return sizeof(T) == 8 ? (J <= 4 ? 3 : 2) : (J <= 2 ? 4 : (J <= 8 ? 3 : 2));
   return sizeof(T) == 8 ? (J <= 4 ? 4 : (J <= 10 ? 3 : 2)) : (J <= 2 ? 5 : (J <= 8 ? 4 : (J <= 10 ? 3 : 2)));
 }

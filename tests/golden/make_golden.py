@@ -441,6 +441,60 @@ def make_burgers(out):
         out[f"bur{N}_win"] = np.stack([lo, hi])
 
 
+def make_burgers_chain(out):
+    """Burgers chains through the reference sampler (burgers_beta.py:25-128's
+    study at N=32): G = Measurer(RusanovFVM.integrate(PerturbedRiemannIC(
+    prior_mean + u))), data = G at the ground truth (burgers_beta.py:116,
+    no noise added), noise γ = 0.05, prior N(0, 0.25²).  Two compositions:
+    pCN (β = 0.15, burgers.org:222-231) and the study's own RW path,
+    VarStepStandardRWProposer(PWLinear) + CountedAccepter(StandardRWAccepter)
+    inside ConstrainAccepter(is_valid_IC) (burgers_wasserstein_chain.py:47-55)."""
+    N = 32
+    prior_mean = np.array([1.5, 0.25, -0.5])  # burgers_beta.py:64-67
+    truth = np.array([0.025, -0.025, -0.02])  # burgers_beta.py:31-35
+    points = np.array([-0.5, -0.25, 0.25, 0.5, 0.75])
+    interval, gamma, sigma_p = 0.1, 0.05, 0.25
+
+    def measure(theta):
+        w, t, n, x, dx = ref_integrate(N, (-1, 1), theta, 1.0)
+        xv = x[1:-1]
+        lo = np.searchsorted(xv, points - interval / 2, side="left")
+        hi = np.searchsorted(xv, points + interval / 2, side="left")
+        return np.array([10 * np.trapz(w[a:b], dx=xv[1] - xv[0]) for a, b in zip(lo, hi)])  # utilities.py:100-109
+
+    def G(u):  # FVMObservationOperator (utilities.py:17-41): evaluated at prior_mean + u
+        return measure(prior_mean + u)
+
+    y = measure(truth)
+
+    def is_valid_IC(u):  # burgers_wasserstein_chain.py:47-55
+        s = u[2] + prior_mean[2]
+        return bool(-1 < s < 1)
+
+    seed = 2024
+    noise = np.full(5, gamma**2)
+    prior_var = np.full(3, sigma_p**2)
+    res = []
+    for chain in range(3):
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, noise, prior_var, 0.15, np.zeros(3), seed, chain, n_samples=5, burn_in=10, interval=4)
+        res.append((s, calls, accepts))
+    out["bch_pcn_samples"] = np.stack([r[0] for r in res])
+    out["bch_pcn_counts"] = np.array([[r[1], r[2]] for r in res])
+    res = []
+    for chain in range(3):
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, noise, prior_var, None, np.zeros(3), seed + 1, chain, n_samples=5, burn_in=10, interval=4,
+            box=is_valid_IC, proposer=lambda prior: VarStepStandardRWProposer(pw_linear(0.1, 0.01, 10), prior),
+            rw_accept=True)
+        res.append((s, calls, accepts))
+    out["bch_rw_samples"] = np.stack([r[0] for r in res])
+    out["bch_rw_counts"] = np.array([[r[1], r[2]] for r in res])
+    out["bch_y"], out["bch_prior_mean"] = y, prior_mean
+    # N, gamma, sigma_p, beta, seed, n_samples, burn_in, interval, PWLinear (d_s, d_e, l)
+    out["bch_meta"] = np.array([N, gamma, sigma_p, 0.15, seed, 5, 10, 4, 0.1, 0.01, 10], dtype=np.float64)
+
+
 # ----------------------------------------------- distributions & schedule
 def make_misc(out):
     g = GaussianDistribution(mean=np.array([1.0, -2.0, 0.5]), covariance=np.diag([0.5, 2.0, 1.5]))
@@ -537,6 +591,16 @@ def make_burn_in(out):
 
 
 def main():
+    path = os.path.join(HERE, "reference_golden.npz")
+    if sys.argv[1:]:
+        # regenerate only the named groups, keeping the other arrays of the file
+        z = np.load(path, allow_pickle=False)
+        out = {k: z[k] for k in z.files}
+        for name in sys.argv[1:]:
+            globals()[f"make_{name}"](out)
+        np.savez_compressed(path, **out)
+        print(f"updated {path} ({', '.join(sys.argv[1:])}): {len(out)} arrays, {os.path.getsize(path)} bytes")
+        return
     out = {}
     make_l96(out)
     make_l96_chain(out)
@@ -547,7 +611,7 @@ def main():
     make_burgers(out)
     make_misc(out)
     make_burn_in(out)
-    path = os.path.join(HERE, "reference_golden.npz")
+    make_burgers_chain(out)
     np.savez_compressed(path, **out)
     print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path)} bytes")
 

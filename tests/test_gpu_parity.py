@@ -524,6 +524,50 @@ def test_sampler_rw_matches_reference_fixture(dev, golden, kind):
         assert acc.accepts == int(golden[f"rw_{kind}_counts"][chain, 1])
 
 
+@pytest.mark.parametrize("kind", ["pcn", "rw"])
+def test_sampler_burgers_chain_matches_reference_fixture(dev, golden, kind):
+    """The reference's Burgers study (burgers_beta.py:25-128, N=32, CFL Rusanov =
+    RusanovFVM.integrate) through its own sampler with injected draws, reproduced
+    by MCMCSampler on the GPU: the stack of 3 chains in one launch per block and
+    each chain alone, pCN and the study's RW composition
+    ConstrainAccepter(CountedAccepter(StandardRWAccepter), is_valid_IC) with
+    VarStepStandardRWProposer(PWLinear)."""
+    from ip_mcmc_amd import (BoxConstraint, BurgersOperator, ConstrainAccepter, ConstSteppCNProposer,
+                             CountedAccepter, EvolutionPotential, GaussianDistribution, MCMCSampler, PhiloxRNG,
+                             PWLinear, StandardRWAccepter, VarStepStandardRWProposer, pCNAccepter)
+
+    meta = golden["bch_meta"]
+    N, gamma, sigma_p, beta, seed = int(meta[0]), meta[1], meta[2], meta[3], int(meta[4])
+    n_samples, burn_in, interval = int(meta[5]), int(meta[6]), int(meta[7])
+    pm = golden["bch_prior_mean"]
+    op = BurgersOperator(prior_mean=pm, N=N, T=1.0, dt_mode="cfl", arith="reference")
+    pot = EvolutionPotential(op, golden["bch_y"], GaussianDistribution(np.zeros(5), gamma**2 * np.eye(5)))
+    prior = GaussianDistribution(np.zeros(3), sigma_p**2 * np.eye(3))
+    want = golden[f"bch_{kind}_samples"]
+    counts = golden[f"bch_{kind}_counts"]
+
+    def sampler(chain_offset):
+        if kind == "pcn":
+            inner = CountedAccepter(pCNAccepter(pot))
+            return MCMCSampler(ConstSteppCNProposer(beta, prior), inner, PhiloxRNG(seed),
+                               chain_offset=chain_offset), inner
+        inner = CountedAccepter(StandardRWAccepter(pot, prior))
+        box = BoxConstraint(lower=[-np.inf, -np.inf, -1.0], upper=[np.inf, np.inf, 1.0], offset=pm)
+        prop = VarStepStandardRWProposer(PWLinear(meta[8], meta[9], int(meta[10])), prior)
+        return MCMCSampler(prop, ConstrainAccepter(inner, box), PhiloxRNG(seed + 1), chain_offset=chain_offset), inner
+
+    s, inner = sampler(0)
+    out = s.run(np.zeros((3, 3)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    assert np.array_equal(out, want)
+    assert np.array_equal(np.asarray(inner.accepts), counts[:, 1])
+    assert np.array_equal(np.asarray(inner.calls), counts[:, 0])
+    for chain in range(3):
+        s, inner = sampler(chain)
+        out = s.run(np.zeros(3), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+        assert np.array_equal(out, want[chain])
+        assert inner.accepts == int(counts[chain, 1]) and inner.calls == int(counts[chain, 0])
+
+
 # ------------------------------------------- two-scale Lorenz-96 (§8(f) #4)
 def _ts_ops():
     from ip_mcmc_amd import TwoScaleLorenz96Operator as TS

@@ -292,3 +292,47 @@ def test_constrained_chain_matches_reference_sampler(orc, golden):
     np.testing.assert_array_equal(samples, golden["con_samples"])
     assert np.array_equal(calls, golden["con_counts"][:, 0])
     assert np.array_equal(acc, golden["con_counts"][:, 1])
+
+
+def _bch_blocks(meta):
+    burn_in, interval, n_samples = int(meta[6]), int(meta[7]), int(meta[5])
+    return [max(0, burn_in - interval)] + [interval] * n_samples
+
+
+@pytest.mark.parametrize("kind", ["pcn", "rw"])
+def test_burgers_chain_matches_reference_sampler(orc, golden, kind):
+    """The reference's Burgers study (burgers_beta.py:25-128, N=32) through its own
+    sampler with injected draws: pCN, and VarStepStandardRWProposer(PWLinear) +
+    StandardRWAccepter inside ConstrainAccepter(is_valid_IC) -- the oracle's
+    CFL Rusanov chains reproduce samples, accepts and calls bit for bit."""
+    meta = golden["bch_meta"]
+    N, gamma, sigma_p, beta, seed = int(meta[0]), meta[1], meta[2], meta[3], int(meta[4])
+    op = BurgersOperator(prior_mean=golden["bch_prior_mean"], N=N, T=1.0, dt_mode="cfl", arith="reference")
+    y, ginv, sq = golden["bch_y"], np.full(5, 1 / gamma), np.full(3, sigma_p)
+    U = np.zeros((3, 3))
+    acc = np.zeros(3, dtype=np.int64)
+    calls = np.zeros(3, dtype=np.int64)
+    samples = np.zeros((3, int(meta[5]), 3))
+    step = 0
+    if kind == "pcn":
+        phi = orc.potential(op, U, y, ginv)
+        for b, n in enumerate(_bch_blocks(meta)):
+            orc.pcn_sweep(op, U, phi, y, ginv, sq, beta, seed, step, n, accepts=acc, calls=calls)
+            step += n
+            if b > 0:
+                samples[:, b - 1] = U
+    else:
+        phi = orc.init_phi(op, U, y, ginv, reg_scale=sq)
+        d_s, d_e, l = meta[8], meta[9], meta[10]
+        box = (np.array([-np.inf, -np.inf, -1.0]), np.array([np.inf, np.inf, 1.0]), golden["bch_prior_mean"])
+        for b, n in enumerate(_bch_blocks(meta)):
+            d = [d_e if i > l else d_s - (d_s - d_e) / l * i for i in range(step + 1, step + n + 1)]
+            sched = np.stack([np.sqrt(2) * np.sqrt(np.array(d)), np.ones(n)], axis=1)
+            orc.pcn_sweep(op, U, phi, y, ginv, sq, 0.0, seed + 1, step, n, accepts=acc, calls=calls, box=box,
+                          beta_schedule=sched, proposal="rw", reg_scale=sq)
+            step += n
+            if b > 0:
+                samples[:, b - 1] = U
+    np.testing.assert_array_equal(samples, golden[f"bch_{kind}_samples"])
+    assert np.array_equal(calls, golden[f"bch_{kind}_counts"][:, 0])
+    assert np.array_equal(acc, golden[f"bch_{kind}_counts"][:, 1])

@@ -111,9 +111,11 @@ def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
         res["lanes_forced"] = lanes
     if spec is not None:
         res["spec_width"] = spec
-    if isinstance(op, Lorenz96Operator):
-        res["lanes_per_chain"] = lib().ipmc_auto_lanes(C.byref(m), adt, n)
-        res["auto_layout"] = lib().ipmc_auto_layout(C.byref(m), adt, n)  # chains_per_lane * 100 + lanes
+    # the kernel plan this sweep ran (ipmc_plan_sweep: the launch's own code path)
+    p = _abi.IpmcPlan()
+    call("ipmc_plan_sweep", C.byref(m), C.byref(s), C.byref(p))
+    res["plan"] = {"lanes_per_chain": p.lanes_per_chain, "chains_per_lane": p.chains_per_lane,
+                   "spec_width": p.spec_width}
     print(json.dumps(res), flush=True)
 
 
