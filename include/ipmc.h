@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 6
+#define IPMC_ABI_VERSION 7
 
 typedef enum {
   IPMC_OK = 0,
@@ -134,7 +134,7 @@ typedef struct ipmc_sweep {
                                = the inner CountedAccepter's calls under ConstrainAccepter(CountedAccepter(..)) */
   const void* y;            /* [q] data */
   const void* gamma_inv;    /* [q] 1/γ_i, diagonal noise covariance Γ = diag(γ²) */
-  const void* prior_sqrt;   /* [k] sqrt of the diagonal prior covariance */
+  const void* prior_sqrt;   /* [k] sqrt of the diagonal prior covariance (NULL if prior_chol is set) */
   const void* box_lo;       /* [k] or NULL: ConstrainAccepter box, valid iff lo < v+off < hi for all i */
   const void* box_hi;       /* [k] or NULL */
   const void* box_off;      /* [k] or NULL (treated as 0) */
@@ -156,6 +156,9 @@ typedef struct ipmc_sweep {
   int64_t sample_stride;
   double* sum_u;            /* optional [n_chains, k] running sum of u after every step (f64) */
   double* sum_u2;           /* optional [n_chains, k] running sum of u^2 */
+  const void* prior_chol;   /* optional [k, k] row-major lower Cholesky factor L of a NON-diagonal prior covariance
+                               (GaussianDistribution.L): w_j = sum_{i<=j} L[j][i] xi_i in ascending i, overriding
+                               prior_sqrt (which may then be NULL); proposer.py:81-82's w ~ N(0, C) */
 } ipmc_sweep;
 
 /* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */

@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -82,6 +82,7 @@ class IpmcSweep(C.Structure):
         ("sample_stride", C.c_int64),
         ("sum_u", C.c_void_p),
         ("sum_u2", C.c_void_p),
+        ("prior_chol", C.c_void_p),
     ]
 
 

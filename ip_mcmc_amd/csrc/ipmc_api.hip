@@ -419,8 +419,8 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
     }
     return IPMC_OK;
   }
-  if (!s->u || !s->phi || !s->y || !s->gamma_inv || !s->prior_sqrt)
-    return fail(IPMC_ERR_INVALID, "u / phi / y / gamma_inv / prior_sqrt is NULL");
+  if (!s->u || !s->phi || !s->y || !s->gamma_inv || (!s->prior_sqrt && !s->prior_chol))
+    return fail(IPMC_ERR_INVALID, "u / phi / y / gamma_inv / prior_sqrt (or prior_chol) is NULL");
   if (s->sample_out && s->sample_stride < m->k) return fail(IPMC_ERR_INVALID, "sample_stride < k");
   if (s->sum_u2 && !s->sum_u) return fail(IPMC_ERR_INVALID, "sum_u2 needs sum_u");
   hipStream_t st = (hipStream_t)stream;

@@ -164,7 +164,8 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
     const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
     const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
     T v[M];
-    pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw);
+    pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw,
+                      (const T*)s.prior_chol, D);
     if (box_valid<T, M, LPC>(s, c0, v, lane)) {
       ++ncalls;
       const T reg = s.reg_scale
@@ -258,7 +259,8 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
       const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
       T v[M];
-      pcn_propose<T, M>(ur, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw);
+      pcn_propose<T, M>(ur, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw,
+                        (const T*)s.prior_chol, D);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][t] = v[j];
       ok = box_valid<T, M, LPC>(s, c0, v, lane);
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     bool oka, okb;
     {
       float va[M];
-      pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va, rw);
+      pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va, rw, (const float*)s.prior_chol, D);
       oka = box_valid<float, M, LPC>(s, c0, va, lane);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].x = va[j];
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     asm volatile("" ::: "memory");
     {
       float vb[M];
-      pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb, rw);
+      pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb, rw, (const float*)s.prior_chol, D);
       okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].y = vb[j];

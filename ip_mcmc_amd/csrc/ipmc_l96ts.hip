@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
       const uint64_t step = s.step0 + (uint64_t)tt;
       const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw);
+      pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw, (const T*)s.prior_chol, 3);
       ok = true;
       if (s.box_lo || s.box_hi) {
         const T* lo = (const T*)s.box_lo;

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
   T* __restrict__ u = (T*)s.u + chain * k;
   const T* sq = (const T*)s.prior_sqrt;
+  const T* chol = (const T*)s.prior_chol;
   const T* lo = (const T*)s.box_lo;
   const T* hi = (const T*)s.box_hi;
   const T* off = (const T*)s.box_off;
@@ -120,14 +121,33 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
     const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
     double z0 = 0.0, z1 = 0.0;
     bool ok = true;
-    for (int j = 0; j < k; ++j) {
-      if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
-      const T w = sq[j] * (T)((j & 1) ? z1 : z0);
-      const T vj = propose_one<T>(rw, u[j], w, cs, bs);
-      v[j * kSmallBlock] = vj;
-      const T t = vj + (off ? off[j] : (T)0);
-      if (lo && !(lo[j] < t)) ok = false;
-      if (hi && !(t < hi[j])) ok = false;
+    if (chol) {
+      // non-diagonal prior (chol_propose's order): ξ parked first, then
+      // w_j = Σ_{i<=j} L[j][i] ξ_i for descending j, each v_j replacing ξ_j
+      for (int j = 0; j < k; j += 2) {
+        normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+        v[j * kSmallBlock] = (T)z0;
+        if (j + 1 < k) v[(j + 1) * kSmallBlock] = (T)z1;
+      }
+      for (int j = k - 1; j >= 0; --j) {
+        T w = (T)0;
+        for (int i = 0; i <= j; ++i) w = w + v[i * kSmallBlock] * chol[(int64_t)j * k + i];
+        const T vj = propose_one<T>(rw, u[j], w, cs, bs);
+        v[j * kSmallBlock] = vj;
+        const T t = vj + (off ? off[j] : (T)0);
+        if (lo && !(lo[j] < t)) ok = false;
+        if (hi && !(t < hi[j])) ok = false;
+      }
+    } else {
+      for (int j = 0; j < k; ++j) {
+        if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+        const T w = sq[j] * (T)((j & 1) ? z1 : z0);
+        const T vj = propose_one<T>(rw, u[j], w, cs, bs);
+        v[j * kSmallBlock] = vj;
+        const T t = vj + (off ? off[j] : (T)0);
+        if (lo && !(lo[j] < t)) ok = false;
+        if (hi && !(t < hi[j])) ok = false;
+      }
     }
     if (ok) {
       ++ncalls;
@@ -218,6 +238,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   const uint64_t gid = (uint64_t)(s.chain_offset + chain);
   T* __restrict__ u = (T*)s.u + chain * k;
   const T* sq = (const T*)s.prior_sqrt;
+  const T* chol = (const T*)s.prior_chol;
   const T* lo = (const T*)s.box_lo;
   const T* hi = (const T*)s.box_hi;
   const T* off = (const T*)s.box_off;
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   for (int j = 0; j < kSpecKMax; ++j) {
     const bool in = j < k;
     ur[j] = in ? u[j] : (T)0;
-    sqr[j] = in ? sq[j] : (T)0;
+    sqr[j] = (in && sq) ? sq[j] : (T)0;
     lor[j] = (in && lo) ? lo[j] : (T)0;
     hir[j] = (in && hi) ? hi[j] : (T)0;
     offr[j] = (in && off) ? off[j] : (T)0;
@@ -253,11 +274,27 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
       double z0 = 0.0, z1 = 0.0;
       ok = true;
+      T xi[kSpecKMax];
+      if (chol) {
+#pragma unroll
+        for (int j = 0; j < kSpecKMax; j += 2) {
+          if (j < k) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+          xi[j] = (T)z0;
+          xi[j + 1] = (T)z1;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < kSpecKMax; ++j) {
         if (j < k) {
-          if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
-          const T w = sqr[j] * (T)((j & 1) ? z1 : z0);
+          T w;
+          if (chol) {  // non-diagonal prior: chol_propose's order
+            w = (T)0;
+#pragma unroll
+            for (int i = 0; i <= j; ++i) w = w + xi[i] * chol[j * k + i];
+          } else {
+            if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+            w = sqr[j] * (T)((j & 1) ? z1 : z0);
+          }
           const T vj = propose_one<T>(rw, ur[j], w, cs, bs);
           v[j * kSpecBlock] = vj;
           const T tb = vj + offr[j];  // + 0 when there is no offset: the same bits as vj

@@ -19,10 +19,42 @@ __device__ __forceinline__ T propose_one(bool rw, T u, T w, T contr, T beta) {
   return rw ? u + beta * w : contr * u + beta * w;
 }
 
+// Non-diagonal prior (sweep.prior_chol = L, the lower Cholesky factor of C,
+// row-major [k, k]): w_j = Σ_{i<=j} L[j][i] ξ_i, summed in ascending i from
+// +0 with no FMA (oracle/orc_models.inc: the same order).  The group's lane
+// owning components [c0, c0+M) draws ξ_0 .. ξ_{c0+M-1} itself (the proposal is
+// a negligible part of a step next to G).
+template <typename T, int M>
+__device__ __forceinline__ void chol_propose(const T* __restrict__ u, const T* __restrict__ L, int k, T contr,
+                                             T beta, uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M],
+                                             bool rw) {
+  T w[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) w[j] = (T)0;
+  const int iend = c0 + M;
+  for (int i = 0; i < iend; i += 2) {
+    double z0, z1;
+    normal_pair(seed, gid, step, (uint32_t)(i >> 1), z0, z1);
+    const T x0 = (T)z0, x1 = (T)z1;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int r = c0 + j;
+      if (i <= r) w[j] = w[j] + x0 * L[(int64_t)r * k + i];
+      if (i + 1 <= r) w[j] = w[j] + x1 * L[(int64_t)r * k + i + 1];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < M; ++j) v[j] = propose_one<T>(rw, u[j], w[j], contr, beta);
+}
+
 template <typename T, int M>
 __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __restrict__ sq, T contr, T beta,
                                             uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M],
-                                            bool rw = false) {
+                                            bool rw = false, const T* __restrict__ chol = nullptr, int k = 0) {
+  if (chol) {
+    chol_propose<T, M>(u, chol, k, contr, beta, seed, gid, step, c0, v, rw);
+    return;
+  }
   if constexpr (M % 2 == 0) {
     // c0 is even whenever M is even: pairs never straddle lanes
 #pragma unroll

@@ -115,7 +115,9 @@ void forward(const at::Tensor& u, at::Tensor g, int64_t model, int64_t stream) {
            "ipmc_forward");
 }
 
-int64_t abi_version() { return ipmc_abi_version(); }
+// the header this front end was compiled against (torch_ops.load() compares it
+// with the ctypes mirror, so a stale build that would pass stale structs raises)
+int64_t abi_version() { return IPMC_ABI_VERSION; }
 
 }  // namespace
 

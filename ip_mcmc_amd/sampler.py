@@ -61,11 +61,14 @@ class _Plan:
                 "device sampler needs a ConstSteppCNProposer, VarSteppCNProposer, ConstStepStandardRWProposer or "
                 f"VarStepStandardRWProposer, not {type(proposer).__name__}"
             )
-        if not proposer.w.is_diagonal:
-            raise UnsupportedOnDevice("device sampler needs a diagonal prior covariance")
         self.proposer = proposer
         self.proposal = _abi.PROPOSAL_RW if proposer.kind == "rw" else _abi.PROPOSAL_PCN
-        self.prior_sqrt = proposer.w.sqrt_diagonal
+        # w ~ N(0, C): sqrt(C_ii)·ξ_i for a diagonal C, else L·ξ with L the lower
+        # Cholesky factor (ipmc_sweep.prior_chol)
+        if proposer.w.is_diagonal:
+            self.prior_sqrt, self.prior_chol = proposer.w.sqrt_diagonal, None
+        else:
+            self.prior_sqrt, self.prior_chol = None, proposer.w.L
         self.counted_outer = []  # CountedAccepters that see every step
         self.counted_inner = []  # CountedAccepters inside a ConstrainAccepter
         self.box = None
@@ -103,8 +106,8 @@ class _Plan:
         self.potential = pot
         self.G = pot.G
         self.y_eff, self.gamma_inv = pot.device_terms()
-        if self.prior_sqrt.shape[0] != self.G.k:
-            raise ValueError(f"prior dimension {self.prior_sqrt.shape[0]} != forward map k = {self.G.k}")
+        if proposer.w.k != self.G.k:
+            raise ValueError(f"prior dimension {proposer.w.k} != forward map k = {self.G.k}")
         if self.reg_scale is not None and self.reg_scale.shape[0] != self.G.k:
             raise ValueError("StandardRWAccepter prior dimension != forward map k")
 
@@ -198,8 +201,9 @@ class MCMCSampler:
         calls = torch.zeros((n_chains,), dtype=torch.int64, device=device) if plan.counted_inner else None
         y_t = dev.to_device(plan.y_eff, td, device)
         gi_t = dev.to_device(plan.gamma_inv, td, device)
-        sq_t = dev.to_device(plan.prior_sqrt, td, device)
-        keep_alive = [y_t, gi_t, sq_t]
+        sq_t = None if plan.prior_sqrt is None else dev.to_device(plan.prior_sqrt, td, device)
+        chol_t = None if plan.prior_chol is None else dev.to_device(plan.prior_chol, td, device)
+        keep_alive = [y_t, gi_t, sq_t, chol_t]
         box_ptrs = (None, None, None)
         if plan.box is not None:
             arrs = plan.box.arrays(k)
@@ -222,7 +226,8 @@ class MCMCSampler:
         sw.calls = dev.ptr(calls)
         sw.y = y_t.data_ptr()
         sw.gamma_inv = gi_t.data_ptr()
-        sw.prior_sqrt = sq_t.data_ptr()
+        sw.prior_sqrt = dev.ptr(sq_t)
+        sw.prior_chol = dev.ptr(chol_t)
         sw.box_lo, sw.box_hi, sw.box_off = box_ptrs
         sw.proposal = plan.proposal
         sw.reg_scale = dev.ptr(reg_t)

@@ -31,6 +31,12 @@ def load():
             raise RuntimeError(f"{TORCH_LIB_PATH} not found; build it with __graft_entry__.build()")
         _ipmc_lib()  # libipmc.so first (the ABI version check lives there)
         torch.ops.load_library(TORCH_LIB_PATH)
+        from . import _abi
+
+        v = int(torch.ops.ipmc.abi_version())
+        if v != _abi.ABI_VERSION:
+            raise RuntimeError(f"libipmc_torch.so was built against ABI {v}, the package is ABI {_abi.ABI_VERSION}: "
+                               "rebuild it with __graft_entry__.build()")
         _loaded = True
     return torch.ops.ipmc
 

@@ -88,7 +88,7 @@ int orc_potential(const ipmc_model* m, int32_t dtype, int64_t n, const void* u, 
 int orc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, int32_t n_threads) {
   int st = check_model(m);
   if (st) return st;
-  if (!s || !s->u || !s->phi || !s->y || !s->gamma_inv || !s->prior_sqrt) return IPMC_ERR_INVALID;
+  if (!s || !s->u || !s->phi || !s->y || !s->gamma_inv || (!s->prior_sqrt && !s->prior_chol)) return IPMC_ERR_INVALID;
   if (s->proposal == IPMC_PROPOSAL_PCN && !(s->beta >= 0.0 && s->beta <= 1.0)) return IPMC_ERR_INVALID;
   const int64_t C = s->n_chains;
   if (n_threads < 1) n_threads = 1;

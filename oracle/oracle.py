@@ -131,10 +131,12 @@ def pcn_sweep(
     n_threads=1,
     proposal="pcn",
     reg_scale=None,
+    prior_chol=None,
 ):
     """In-place sweep on numpy arrays U [C, k] and phi [C] (dtype from U).
     proposal 'pcn': v = sqrt(1-beta^2) u + beta w; 'rw': v = u + beta w.
-    reg_scale: StandardRWAccepter regularizer scale (phi then holds I)."""
+    reg_scale: StandardRWAccepter regularizer scale (phi then holds I).
+    prior_chol: [k, k] lower Cholesky factor of a non-diagonal prior (w = L·ξ)."""
     npd = U.dtype.type
     assert U.flags.c_contiguous and phi.dtype == U.dtype
     m, keep = model_struct(op, npd)
@@ -142,8 +144,9 @@ def pcn_sweep(
     y, gi, sq = cv(y), cv(ginv), cv(prior_sqrt)
     lo, hi, off = (cv(b) for b in box)
     rs = cv(reg_scale)
+    ch = cv(prior_chol)
     sched = None if beta_schedule is None else np.ascontiguousarray(beta_schedule, dtype=np.float64)
-    keep += [y, gi, sq, lo, hi, off, sched, rs]
+    keep += [y, gi, sq, lo, hi, off, sched, rs, ch]
     s = _abi.IpmcSweep()
     s.dtype = _abi_dtype(npd)
     s.n_chains = U.shape[0]
@@ -159,6 +162,7 @@ def pcn_sweep(
     s.beta_schedule = _p(sched)
     s.proposal = _abi.PROPOSAL_RW if proposal == "rw" else _abi.PROPOSAL_PCN
     s.reg_scale = _p(rs)
+    s.prior_chol = _p(ch)
     s.seed = seed
     s.step0 = step0
     s.n_steps = n_steps

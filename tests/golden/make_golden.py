@@ -78,8 +78,18 @@ class CounterRNG(np.random.Generator):
         k = len(mean)
         xi = O.normals(self.s, self.chain, 1, self.step, k)[0]
         cov = np.asarray(cov)
-        assert np.all(cov == np.diag(np.diag(cov))), "harness handles diagonal covariances"
-        return np.sqrt(np.diag(cov)) * xi + mean
+        if np.all(cov == np.diag(np.diag(cov))):
+            return np.sqrt(np.diag(cov)) * xi + mean
+        # a non-diagonal covariance: L·ξ with L = cholesky(C), summed in the
+        # device's order (include/ipmc.h prior_chol: ascending i from +0)
+        L = np.linalg.cholesky(cov)
+        w = np.zeros(k)
+        for j in range(k):
+            acc = 0.0
+            for i in range(j + 1):
+                acc = acc + float(xi[i]) * float(L[j, i])
+            w[j] = acc
+        return w + mean
 
     def random(self):
         self.uniform_steps.append(self.step)
@@ -100,8 +110,9 @@ class RecordingAccepter:
 
 
 def run_reference_chain(G, y, noise_cov_diag, prior_var_diag, beta, u0, seed, chain, n_samples, burn_in, interval,
-                        box=None, proposer=None, rw_accept=False):
-    prior = GaussianDistribution(mean=np.zeros(len(u0)), covariance=np.diag(prior_var_diag))
+                        box=None, proposer=None, rw_accept=False, prior_cov=None):
+    cov = np.diag(prior_var_diag) if prior_cov is None else np.asarray(prior_cov)
+    prior = GaussianDistribution(mean=np.zeros(len(u0)), covariance=cov)
     noise = GaussianDistribution(mean=np.zeros(len(y)), covariance=np.diag(noise_cov_diag))
     pot = EvolutionPotential(G, y, noise)
     prop = ConstSteppCNProposer(beta, prior) if proposer is None else proposer(prior)
@@ -495,6 +506,55 @@ def make_burgers_chain(out):
     out["bch_meta"] = np.array([N, gamma, sigma_p, 0.15, seed, 5, 10, 4, 0.1, 0.01, 10], dtype=np.float64)
 
 
+def make_dense_prior(out):
+    """pCN with a NON-diagonal prior covariance through the reference sampler
+    (proposer.py:59-82: w ~ N(0, C) drawn by GaussianDistribution.sample,
+    distribution.py:114-118), the draws injected as L·ξ: the linear problem of
+    config 1 with an AR(1) prior, and the Lorenz-96 K=8 chain problem with a
+    periodic squared-exponential prior on the forcing field."""
+    g = np.array([3.0, 1.0, 4.0, 1.0])
+    gamma = 0.5
+    y = np.array([np.dot(g, [2.0, 7.0, 1.0, 8.0]) + 0.3])
+    idx = np.arange(4)
+    cov = 0.8 ** np.abs(idx[:, None] - idx[None, :])
+    seed = 5150
+
+    def G(u):
+        return np.dot(g, u)
+
+    res = []
+    for chain in range(3):
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G, y, np.array([gamma**2]), None, 0.5, np.zeros(4), seed, chain, n_samples=30, burn_in=60, interval=10,
+            prior_cov=cov)
+        res.append((s, accepts))
+    out["dpl_cov"], out["dpl_g"], out["dpl_y"] = cov, g, y
+    out["dpl_meta"] = np.array([gamma, 0.5, seed, 30, 60, 10], dtype=np.float64)
+    out["dpl_samples"] = np.stack([r[0] for r in res])
+    out["dpl_accepts"] = np.array([r[1] for r in res])
+
+    K, n, dt = 8, 100, 0.01
+    x0, y96 = out["l96c_x0"], out["l96c_y"]
+    d = np.abs(np.arange(K)[:, None] - np.arange(K)[None, :])
+    d = np.minimum(d, K - d)
+    cov96 = np.exp(-0.5 * (d / 1.2) ** 2) + 0.05 * np.eye(K)
+    fm = np.full(K, 8.0)
+    seed96 = 0x5EED
+    res = []
+    for chain in range(3):
+        def G96(u):
+            return rk4_time_average(l96_ref_rhs(K, fm + u), x0, dt, n)
+
+        s, dec, steps, calls, accepts = run_reference_chain(
+            G96, y96, np.full(K, 0.1**2), None, 0.3, np.zeros(K), seed96, chain, n_samples=6, burn_in=20, interval=10,
+            prior_cov=cov96)
+        res.append((s, accepts))
+    out["dp96_cov"] = cov96
+    out["dp96_meta"] = np.array([K, n, dt, 0.1, 0.3, seed96, 6, 20, 10], dtype=np.float64)
+    out["dp96_samples"] = np.stack([r[0] for r in res])
+    out["dp96_accepts"] = np.array([r[1] for r in res])
+
+
 # ----------------------------------------------- distributions & schedule
 def make_misc(out):
     g = GaussianDistribution(mean=np.array([1.0, -2.0, 0.5]), covariance=np.diag([0.5, 2.0, 1.5]))
@@ -612,6 +672,7 @@ def main():
     make_misc(out)
     make_burn_in(out)
     make_burgers_chain(out)
+    make_dense_prior(out)
     np.savez_compressed(path, **out)
     print(f"wrote {path}: {len(out)} arrays, {os.path.getsize(path)} bytes")
 

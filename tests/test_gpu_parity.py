@@ -86,7 +86,8 @@ def test_forward_and_potential_bit_exact(dev, orc, dtype):
 
 # ----------------------------------------------------------------- sweep
 def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, dev, lanes=0, box=None,
-                  sched=None, chain_offset=0, want_sums=False, cpl=0, proposal="pcn", reg_scale=None, spec=1):
+                  sched=None, chain_offset=0, want_sums=False, cpl=0, proposal="pcn", reg_scale=None, spec=1,
+                  chol=None):
     """One ipmc_pcn_sweep launch.  spec=1 (default) runs the sequential kernels;
     spec=0 lets the library choose a speculation width, >1 forces one."""
     from ip_mcmc_amd import _abi
@@ -109,6 +110,10 @@ def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, 
     s.u, s.phi, s.accepts, s.calls = U.data_ptr(), phi.data_ptr(), acc.data_ptr(), calls.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = yt.data_ptr(), gt.data_ptr(), st.data_ptr()
     keep = []
+    if chol is not None:  # non-diagonal prior: the factor replaces prior_sqrt
+        ct = _t(chol, dtype, dev)
+        keep.append(ct)
+        s.prior_chol, s.prior_sqrt = ct.data_ptr(), None
     if box is not None:
         bt = [None if b is None else _t(b, dtype, dev) for b in box]
         keep += bt
@@ -138,7 +143,7 @@ def _sweep_device(op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, 
 
 
 def _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dtype, box=None, sched=None,
-                  chain_offset=0, want_sums=False, proposal="pcn", reg_scale=None):
+                  chain_offset=0, want_sums=False, proposal="pcn", reg_scale=None, chol=None):
     npd = _np(dtype)
     U = np.ascontiguousarray(U0.astype(npd))
     phi = np.ascontiguousarray(phi0.astype(npd))
@@ -147,7 +152,7 @@ def _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, seed, step0, n_steps, dt
     sums = (np.zeros(U.shape), np.zeros(U.shape)) if want_sums else None
     orc.pcn_sweep(op, U, phi, y, ginv, sq, beta, seed, step0, n_steps, accepts=acc, calls=calls,
                   chain_offset=chain_offset, box=box or (None, None, None), beta_schedule=sched, sums=sums,
-                  n_threads=8, proposal=proposal, reg_scale=reg_scale)
+                  n_threads=8, proposal=proposal, reg_scale=reg_scale, prior_chol=chol)
     out = dict(u=U, phi=phi, acc=acc, calls=calls)
     if want_sums:
         out["sum_u"], out["sum_u2"] = sums
@@ -800,3 +805,88 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
         d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, spec=widths[-1], proposal="rw",
                           reg_scale=rs)
         _assert_same(d, o, (type(op).__name__, "rw"))
+
+
+# ------------------------------------------------ non-diagonal priors (L·ξ)
+def _dense_chol(k, seed):
+    """A random SPD prior covariance's lower Cholesky factor (correlated components)."""
+    rng = np.random.default_rng(seed)
+    A = rng.normal(size=(k, k)) / np.sqrt(k)
+    C = 0.3 * np.eye(k) + A @ A.T
+    return np.linalg.cholesky(C)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_dense_prior_every_kernel_family_bit_exact(dev, orc, dtype):
+    """prior_chol (w = L·ξ, include/ipmc.h) in every sweep kernel family vs the
+    oracle: Lorenz-96 (DPP / LDS layouts, packed fp32 pairs, speculation in a
+    wave and over a block), Lorenz-63 and linear (one lane per chain and
+    speculative slots; linear k = 12 beyond the speculative kernel's k <= 8),
+    Burgers and two-scale Lorenz-96 (k = 3); pCN and RW, with a box."""
+    from ip_mcmc_amd import (BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator,
+                             TwoScaleLorenz96Operator)
+
+    rng = np.random.default_rng(4)
+    cases = [
+        (Lorenz96Operator(40, 8.0, dt=0.005, n_steps=40), dict(lanes=4), 131, 5),
+        (Lorenz96Operator(40, 8.0, dt=0.005, n_steps=40, arith="reference"), dict(lanes=8), 131, 5),
+        (Lorenz96Operator(8, 8.0, dt=0.005, n_steps=40), dict(lanes=2, cpl=2 if dtype == torch.float32 else 0), 131,
+         5),
+        (Lorenz96Operator(40, 8.0, dt=0.005, n_steps=40), dict(spec=0), 3, 40),  # auto: block-wide slots
+        (Lorenz96Operator(16, 8.0, dt=0.005, n_steps=40), dict(spec=8, lanes=4), 17, 30),
+        (Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=100), dict(), 200, 12),
+        (Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=100), dict(spec=0), 50, 40),
+        (LinearOperator(rng.normal(size=(3, 12)), rng.normal(size=12)), dict(), 200, 12),
+        (LinearOperator(rng.normal(size=(2, 7)), rng.normal(size=7)), dict(spec=16), 40, 40),
+        (BurgersOperator(N=64, dt_mode="fixed", dt=2e-3, n_steps=150), dict(), 70, 4),
+        (TwoScaleLorenz96Operator(K=6, J=4, x0=rng.normal(size=30), dt=0.004, n_steps=40), dict(), 70, 6),
+    ]
+    for i, (op, kw, n, steps) in enumerate(cases):
+        U0, phi0, y, ginv, sq = _problem(op, n, dtype, orc, seed=i)
+        L = 0.4 * _dense_chol(op.k, i)
+        for proposal in ("pcn", "rw"):
+            box = None
+            if i == 5:  # a box on one component of Lorenz-63
+                box = (np.array([-np.inf, -0.6, -np.inf]), np.array([np.inf, 0.6, np.inf]), None)
+            d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 500 + i, 3, steps, dtype, dev, chol=L,
+                              proposal=proposal, box=box, **kw)
+            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 500 + i, 3, steps, dtype, chol=L,
+                              proposal=proposal, box=box)
+            _assert_same(d, o, (type(op).__name__, kw, proposal))
+            assert np.array_equal(d["samp"], o["u"])
+            assert o["acc"].sum() > 0, (type(op).__name__, proposal)
+
+
+def test_dense_prior_diagonal_factor_equals_diagonal_path(dev, orc):
+    """A diagonal L through prior_chol gives the bits of prior_sqrt (0 + p = p)."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=40)
+    U0, phi0, y, ginv, sq = _problem(op, 64, torch.float64, orc, seed=9)
+    a = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 42, 0, 6, torch.float64, dev)
+    b = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 42, 0, 6, torch.float64, dev, chol=np.diag(sq))
+    _assert_same(a, b, "diag")
+
+
+@pytest.mark.parametrize("case", ["linear", "l96"])
+def test_sampler_dense_prior_matches_reference_fixture(dev, golden, case):
+    """MCMCSampler with a non-diagonal prior GaussianDistribution reproduces the
+    reference sampler's chains (proposer.py:59-82, injected L·ξ draws)."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             LinearOperator, Lorenz96Operator, MCMCSampler, PhiloxRNG, pCNAccepter)
+
+    if case == "linear":
+        gamma, beta, seed, n_samples, burn_in, interval = golden["dpl_meta"]
+        op = LinearOperator(golden["dpl_g"], arith="reference")
+        y, cov, key = golden["dpl_y"], golden["dpl_cov"], "dpl"
+    else:
+        K, n, dt, gamma, beta, seed, n_samples, burn_in, interval = golden["dp96_meta"]
+        op = Lorenz96Operator(int(K), 8.0, x0=golden["l96c_x0"], dt=dt, n_steps=int(n), arith="reference")
+        y, cov, key = golden["l96c_y"], golden["dp96_cov"], "dp96"
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(op.q), gamma**2 * np.eye(op.q)))
+    prior = GaussianDistribution(np.zeros(op.k), cov)
+    acc = CountedAccepter(pCNAccepter(pot))
+    s = MCMCSampler(ConstSteppCNProposer(beta, prior), acc, PhiloxRNG(int(seed)))
+    out = s.run(np.zeros((3, op.k)), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+    assert np.array_equal(out, golden[f"{key}_samples"])
+    assert np.array_equal(np.asarray(acc.accepts), golden[f"{key}_accepts"])

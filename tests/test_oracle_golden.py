@@ -336,3 +336,33 @@ def test_burgers_chain_matches_reference_sampler(orc, golden, kind):
     np.testing.assert_array_equal(samples, golden[f"bch_{kind}_samples"])
     assert np.array_equal(calls, golden[f"bch_{kind}_counts"][:, 0])
     assert np.array_equal(acc, golden[f"bch_{kind}_counts"][:, 1])
+
+
+@pytest.mark.parametrize("case", ["linear", "l96"])
+def test_dense_prior_chain_matches_reference_sampler(orc, golden, case):
+    """A non-diagonal prior covariance (proposer.py:59-82, w ~ N(0, C) from
+    GaussianDistribution.sample) through the reference sampler with injected
+    L·ξ draws: the oracle's prior_chol proposal reproduces samples and accepts."""
+    if case == "linear":
+        gamma, beta, seed, n_samples, burn_in, interval = golden["dpl_meta"]
+        op = LinearOperator(golden["dpl_g"], arith="reference")
+        y, cov, key = golden["dpl_y"], golden["dpl_cov"], "dpl"
+    else:
+        K, n, dt, gamma, beta, seed, n_samples, burn_in, interval = golden["dp96_meta"]
+        op = Lorenz96Operator(int(K), 8.0, x0=golden["l96c_x0"], dt=dt, n_steps=int(n), arith="reference")
+        y, cov, key = golden["l96c_y"], golden["dp96_cov"], "dp96"
+    k = op.k
+    L = np.linalg.cholesky(cov)
+    U = np.zeros((3, k))
+    ginv = np.full(op.q, 1.0 / gamma)
+    phi = orc.potential(op, U, y, ginv)
+    acc = np.zeros(3, dtype=np.int64)
+    step = 0
+    samples = np.zeros((3, int(n_samples), k))
+    for b, nb in enumerate([max(0, int(burn_in) - int(interval))] + [int(interval)] * int(n_samples)):
+        orc.pcn_sweep(op, U, phi, y, ginv, None, beta, int(seed), step, nb, accepts=acc, prior_chol=L)
+        step += nb
+        if b > 0:
+            samples[:, b - 1] = U
+    np.testing.assert_array_equal(samples, golden[f"{key}_samples"])
+    assert np.array_equal(acc, golden[f"{key}_accepts"])
