@@ -52,10 +52,19 @@ def _stream(t, stream):
     return torch.cuda.current_stream(t.device).cuda_stream if stream is None else int(stream)
 
 
+def _require_device(u):
+    """The ops have no CPU kernel: a host tensor raises here, before any
+    model arrays are built for it (torch's dispatcher raises the same for
+    the raw ops)."""
+    if u.device.type != "cuda":
+        raise NotImplementedError(f"torch.ops.ipmc runs on ROCm device tensors only, got a {u.device.type} tensor")
+
+
 def pcn_sweep(op, u, phi, accepts, y, gamma_inv, prior_sqrt, beta, seed, step0, n_steps, chain_offset=0,
               proposal="pcn", sum_u=None, sum_u2=None, stream=None):
     """n_steps pCN (or RW) steps of every chain of u [C, k], in place; see include/ipmc.h ipmc_pcn_sweep."""
     ops = load()
+    _require_device(u)
     contraction = math.sqrt(1.0 - beta * beta) if proposal == "pcn" else 1.0
     ops.pcn_sweep(u, phi, accepts, y, gamma_inv, prior_sqrt, _model_address(op, u.dtype, u.device),
                   float(beta), contraction, int(seed), int(chain_offset), int(step0), int(n_steps),
@@ -65,6 +74,7 @@ def pcn_sweep(op, u, phi, accepts, y, gamma_inv, prior_sqrt, beta, seed, step0, 
 def potential(op, u, y, gamma_inv, stream=None):
     """Φ(u) for u [n, k] (device tensor) -> phi [n]."""
     ops = load()
+    _require_device(u)
     phi = torch.empty(u.shape[0], dtype=u.dtype, device=u.device)
     ops.potential(u, y, gamma_inv, phi, _model_address(op, u.dtype, u.device), _stream(u, stream))
     return phi
@@ -73,6 +83,7 @@ def potential(op, u, y, gamma_inv, stream=None):
 def forward(op, u, stream=None):
     """G(u) for u [n, k] (device tensor) -> g [n, q]."""
     ops = load()
+    _require_device(u)
     g = torch.empty((u.shape[0], op.q), dtype=u.dtype, device=u.device)
     ops.forward(u, g, _model_address(op, u.dtype, u.device), _stream(u, stream))
     return g
