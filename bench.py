@@ -38,6 +38,10 @@ from ip_mcmc_amd import Lorenz96Operator, _abi  # noqa: E402
 from ip_mcmc_amd._lib import call  # noqa: E402
 
 D, N_RK, DT, BETA, GAMMA = 40, 2000, 0.005, 0.2, 0.1
+ITEM = {"f64": 8, "f32": 4}
+# 30 algorithmic FLOP per component and RK4 step in 20 VALU ops (10 of them
+# FMA): at most 30 / (2 x 20) of the all-FMA peak
+MIX_CEILING = 30 / 40
 CHAINS_PER_GPU = 65536
 FLOP_PER_STEP = 30 * D * N_RK  # 2.4e6
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}  # MI355X vector (spec), MI355X_MICROARCH.md
@@ -91,16 +95,20 @@ def sweep_plan(model, sweep):
     return p.lanes_per_chain, p.chains_per_lane, p.spec_width
 
 
-def pmc_traffic(dtype, chains):
-    """HBM bytes per launch of the sweep kernel from the committed rocprofv3
-    PMC passes (profiles/r*/pmc_l96_<dtype>.json: FETCH_SIZE x2 + WRITE_SIZE,
-    corrected as MI355X_MICROARCH.md's HBM section prescribes), or None."""
+def pmc_record(dtype, chains, lanes):
+    """The committed rocprofv3 PMC passes of this sweep kernel (same dtype,
+    chains, shape and lanes-per-chain layout): profiles/r*/pmc_l96_<dtype>.json,
+    newest round first -- HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE,
+    corrected as MI355X_MICROARCH.md's HBM section prescribes), clock and VALU
+    issue rate -- with its path, or (None, None)."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"pmc_l96_{dtype}.json")), reverse=True):
         rec = json.load(open(path))
-        if rec.get("chains") == chains and rec.get("d") == D and rec.get("rk4_steps") == N_RK:
-            return rec["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+        names = " ".join(rec.get("kernel", []))
+        if (rec.get("chains") == chains and rec.get("d") == D and rec.get("rk4_steps") == N_RK
+                and f"{D}, {lanes}, true" in names):
+            return rec, os.path.relpath(path, REPO)
     return None, None
 
 
@@ -251,7 +259,8 @@ def main():
     flop = args.chains * FLOP_PER_STEP
     achieved = flop / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    traffic, traffic_src = pmc_traffic(args.dtype, args.chains)
+    pmc, pmc_src = pmc_record(args.dtype, args.chains, w.lanes)
+    traffic = None if pmc is None else pmc["hbm_bytes_per_launch"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("CPU baseline (C oracle)")
@@ -296,13 +305,20 @@ def main():
                 "frac": achieved / peak,
                 "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC)",
-                "traffic_source": traffic_src,
+                "traffic_source": pmc_src,
+                "algorithmic_bytes": args.chains * (D * ITEM[args.dtype] + 2 * (ITEM[args.dtype] + 8)),
                 "hbm_GBps": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9,
                 "hbm_frac": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "kernel_ms": kern_ms,
                 "flop_per_launch": flop,
-                "note": "vector-ALU (FP64 pipe) bound, no MFMA: algorithmic FLOP = 30*d*n per chain-step; "
-                        "PMC shows the FP64 pipe saturated at ~2.03 GHz (profiles/r1/pmc_l96_f64.json)",
+                "clock_GHz_pmc": None if pmc is None else pmc.get("effective_clock_GHz"),
+                "valu_issue_per_simd_cycle_pmc": None if pmc is None else pmc.get("valu_issue_per_simd_cycle"),
+                "mix_ceiling_frac": MIX_CEILING,
+                "note": "vector-ALU bound (FP64 pipe; packed FP32 for f32), no MFMA and no HBM traffic in the "
+                        "RK loop: algorithmic FLOP = 30*d*n per chain-step, issued as 20 VALU ops of which 10 "
+                        "FMA, so the op mix caps achieved/peak at mix_ceiling_frac (x clock/2.4 GHz); "
+                        "valu_issue_per_simd_cycle 0.25 = a wave64 op every 4 cycles = the pipe issuing every "
+                        "slot (traffic_source holds the PMC passes)",
             },
             "cpu_baseline": cpu,
             "accept_rate": accept_rate,

@@ -38,6 +38,50 @@ __device__ __forceinline__ void l96_rhs(const T (&s)[M], const T (&F)[M], T (&o)
   }
 }
 
+// One classical RK4 stage with every rate consumed as soon as it is computed
+// (no array of rates; cf. ts_stage in ipmc_l96ts.hip):
+//   STAGE 1:   k = f(x);  acc = k;          xs = x + c k
+//   STAGE 2/3: k = f(xs); acc = 2k + acc;   xs = x + c k   (in place)
+//   STAGE 4:   k = f(xs); acc = acc + k;    x = x + c acc;  ob = ob + x
+// The same operations as the textbook form (l96_rhs, then the updates), so the
+// bits do not change.  The stage input's halos are fetched before anything is
+// written, and the old X_{j-1}, X_{j-2} ride along in p1, p2, so `in` may alias
+// `xs`: one array of M values fewer live in the RK loop.
+template <typename V, int M, int LPC, bool FM, int STAGE>
+__device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (&acc)[M], V (&ob)[M],
+                                          const V (&F)[M], V c, V two, int lane) {
+  static_assert(M >= 2, "Lorenz-96 needs at least 2 components per lane");
+  const V sr1 = group_next<LPC>(in[0], lane);
+  V p2 = group_prev<LPC>(in[M - 2], lane);
+  V p1 = group_prev<LPC>(in[M - 1], lane);
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const V cur = in[j];
+    const V xp1 = (j < M - 1) ? in[j + 1] : sr1;
+    V k;
+    if constexpr (FM) {
+      k = madd<true>(xp1 - p2, p1, F[j] - cur);
+    } else {
+      V t = -cur;
+      t = t - (p1 * p2 - p1 * xp1);
+      k = t + F[j];
+    }
+    p2 = p1;
+    p1 = cur;
+    if constexpr (STAGE == 1) {
+      acc[j] = k;
+      xs[j] = madd<FM>(c, k, x[j]);
+    } else if constexpr (STAGE == 4) {
+      acc[j] = acc[j] + k;
+      x[j] = madd<FM>(c, acc[j], x[j]);
+      ob[j] = ob[j] + x[j];
+    } else {
+      acc[j] = madd<FM>(two, k, acc[j]);
+      xs[j] = madd<FM>(c, k, x[j]);
+    }
+  }
+}
+
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
 // V is the per-lane storage type (float, double, or f32x2 = two fp32 chains),
 // S the scalar type of the problem constants.
@@ -55,32 +99,11 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     ob[j] = P::of((S)0);
   }
   for (int n = 0; n < nsteps; ++n) {
-    V k[M], acc[M], xs[M];
-    l96_rhs<V, M, LPC, FM>(x, F, k, lane);
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      acc[j] = k[j];
-      xs[j] = madd<FM>(h2, k[j], x[j]);
-    }
-    l96_rhs<V, M, LPC, FM>(xs, F, k, lane);
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      acc[j] = madd<FM>(two, k[j], acc[j]);
-      xs[j] = madd<FM>(h2, k[j], x[j]);
-    }
-    l96_rhs<V, M, LPC, FM>(xs, F, k, lane);
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      acc[j] = madd<FM>(two, k[j], acc[j]);
-      xs[j] = madd<FM>(h, k[j], x[j]);
-    }
-    l96_rhs<V, M, LPC, FM>(xs, F, k, lane);
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      acc[j] = acc[j] + k[j];
-      x[j] = madd<FM>(h6, acc[j], x[j]);
-      ob[j] = ob[j] + x[j];
-    }
+    V acc[M], xs[M];
+    l96_stage<V, M, LPC, FM, 1>(x, xs, x, acc, ob, F, h2, two, lane);
+    l96_stage<V, M, LPC, FM, 2>(xs, xs, x, acc, ob, F, h2, two, lane);
+    l96_stage<V, M, LPC, FM, 3>(xs, xs, x, acc, ob, F, h, two, lane);
+    l96_stage<V, M, LPC, FM, 4>(xs, xs, x, acc, ob, F, h6, two, lane);
   }
   const V nn = P::of((S)nsteps);
 #pragma unroll
@@ -113,25 +136,40 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
 }
 
 // Occupancy target (waves per SIMD) the register allocator is held to: the
-// state needs ~6 arrays of M values live in the RK loop (x, F, time-average,
-// k-sum, stage, rhs), plus ~40 registers of addressing / RNG / loop state.
+// RK loop keeps 5 arrays of M values live (x, F, time-average, k-sum, stage;
+// l96_stage consumes each rate as it is computed), the proposal / accept stage
+// ~40 registers of addressing / RNG / loop state around it.  The target is
+// sized for 6 arrays: with 5, fp64 M = 20 fits two waves only by spilling
+// ~230 B per lane around every G evaluation (3.6x the compulsory HBM bytes of
+// the headline sweep, profiles/r2/pmc_l96_f64_lpc2_spill.json) for 1 % speed.
 // (fp32 one chain per lane group: the compiler's SLP packing needs ~96; every
-// variant gets at least 96 registers, i.e. at most 5 waves, since the
-// proposal / accept stage spills below that.)
+// variant gets at least 104 registers, i.e. at most 4 waves, since the
+// proposal / accept stage spills below that: 20-56 B per lane at 5 waves for
+// M <= 5, e.g. d=40 at 8 lanes per chain.)
 template <typename T, int M>
 constexpr int l96_waves_per_simd() {
+#ifdef IPMC_L96_WAVES  // occupancy experiments (tools/)
+  return IPMC_L96_WAVES;
+#endif
   constexpr int want = 6 * M * (int)(sizeof(T) / 4) + (sizeof(T) == 8 ? 40 : 96);
-  constexpr int regs = want < 96 ? 96 : want;
+  constexpr int regs = want < 104 ? 104 : want;
   constexpr int w = 512 / regs;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
-// The packed fp32 kernel carries two chains' proposal/accept state (~76
-// registers, measured: <40,4> needs 196 VGPRs); holding it to fewer spills
-// to scratch, so its target is set from 12·M + 76.
+// The packed fp32 kernel: 5 arrays of M f32x2 in the RK loop plus two chains'
+// proposal / accept state (~76 registers); at least 196 registers (<40,4>
+// spills in the proposal stage below that).  Two waves up to M = 17: a 257th
+// register (the dense-prior proposal path pushed <256,16> to 256 VGPRs + 9
+// AGPRs) halves the occupancy of every ensemble larger than one wave per SIMD,
+// e.g. config 5's d=256 (121 -> 110 ms per f32 sweep; profiles/r2).
 template <int M>
 constexpr int l96_pk_waves_per_simd() {
-  constexpr int w = 512 / (12 * M + 76);
+#ifdef IPMC_PK_WAVES  // occupancy experiments (tools/)
+  return IPMC_PK_WAVES;
+#endif
+  constexpr int want = 10 * M + 80;
+  constexpr int w = 512 / (want < 196 ? 196 : want);
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
@@ -159,12 +197,16 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
     // Opaque per-step offset: keeps the loop-invariant per-component constants
     // (theta0, x0, y, 1/gamma, sqrt C) from being hoisted into 5*M VGPRs for
     // the whole launch; they are re-read from L1/L2 once per pCN step instead.
+    // The proposal takes it as its first component too, so the Philox rounds on
+    // the (constant) normal slots are recomputed each step rather than hoisted
+    // and spilled to scratch around G (36 B per lane: 1.6x the compulsory HBM
+    // bytes of the headline sweep, profiles/r2/pmc_l96_f64_hoisted.json).
     int cl = c0;
     asm volatile("" : "+v"(cl));
     const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * st] : beta;
     const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * st + 1] : contr;
     T v[M];
-    pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw,
+    pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, cl, v, rw,
                       (const T*)s.prior_chol, D);
     if (box_valid<T, M, LPC>(s, c0, v, lane)) {
       ++ncalls;
@@ -380,12 +422,18 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     const float cs = s.beta_schedule ? (float)s.beta_schedule[2 * st + 1] : contr;
     const float* sq = (const float*)s.prior_sqrt + cl;
     const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
+    // the proposal's component base: opaque per step (no hoisted, spilled
+    // Philox rounds, as in l96_sweep_kernel) except at M = 20, whose spill-free
+    // register assignment with the hoisted form measured 7 % faster (d=40,
+    // 1.77 vs 1.91 ms; the RK loop's instructions are identical, their VGPR
+    // numbering is not: profiles/r2/pk_codegen.txt)
+    const int pc0 = (M == 20) ? c0 : cl;
     // propose A, park it, then B: one chain's proposal live at a time (the
     // two-chain proposal stage otherwise spills past the occupancy target)
     bool oka, okb;
     {
       float va[M];
-      pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, c0, va, rw, (const float*)s.prior_chol, D);
+      pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, pc0, va, rw, (const float*)s.prior_chol, D);
       oka = box_valid<float, M, LPC>(s, c0, va, lane);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].x = va[j];
@@ -393,7 +441,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     asm volatile("" ::: "memory");
     {
       float vb[M];
-      pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, c0, vb, rw, (const float*)s.prior_chol, D);
+      pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, pc0, vb, rw, (const float*)s.prior_chol, D);
       okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].y = vb[j];

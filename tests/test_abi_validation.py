@@ -163,10 +163,10 @@ def test_diagnostics_checks(h):
 
 def test_auto_layout(h):
     """The layout the sweep picks by itself: fp64 d=40 -> 4 lanes per
-    chain; fp32 -> two chains per lane group as f32x2, 4 lanes; d=256 -> 16 lanes."""
+    chain; fp32 -> two chains per lane group as f32x2, 2 lanes; d=256 -> 16 lanes."""
     m = _model()
     assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 65536) == 104
-    assert h.ipmc_auto_layout(C.byref(m), _abi.F32, 65536) == 204
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F32, 65536) == 202
     assert h.ipmc_auto_lanes(C.byref(m), _abi.F64, 65536) == 4
     m = _model(dim=256, k=256, q=256)
     assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 131072) == 116
@@ -174,12 +174,13 @@ def test_auto_layout(h):
 
 
 # (dim, dtype, chains) -> cpl * 100 + lpc: the measured-fastest layout, or one
-# within 4 % of it, of profiles/r1/lanes_layout_rule.txt
+# within 4 % of it, of profiles/r1/lanes_layout_rule.txt (d=40 at 32 768 and
+# 65 536 chains: profiles/r2/lanes_inplace.txt, after the in-place RK4 stages)
 LAYOUT_TABLE = [
     (8, "f64", 16384, 104), (8, "f64", 65536, 101), (8, "f32", 16384, 104), (8, "f32", 65536, 202),
     (16, "f64", 16384, 104), (16, "f64", 65536, 101), (16, "f32", 16384, 104), (16, "f32", 65536, 202),
     (40, "f64", 8192, 108), (40, "f64", 16384, 104), (40, "f64", 32768, 104), (40, "f64", 65536, 104),
-    (40, "f32", 8192, 108), (40, "f32", 16384, 104), (40, "f32", 32768, 204), (40, "f32", 65536, 204),
+    (40, "f32", 8192, 108), (40, "f32", 16384, 104), (40, "f32", 32768, 204), (40, "f32", 65536, 202),
     (80, "f64", 16384, 104), (80, "f64", 65536, 104), (80, "f32", 16384, 216), (80, "f32", 65536, 204),
     # below one wave per SIMD (speculative sweeps): DPP halos (profiles/r1/l96_small_layouts.jsonl)
     (40, "f64", 1, 104), (40, "f64", 64, 104), (40, "f64", 1024, 104), (40, "f32", 1, 104), (40, "f32", 1024, 104),
@@ -235,7 +236,7 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     s = _sweep(n=65536)
     assert _plan(h, m, s) == (4, 1, 1)  # headline: 4 lanes per chain, sequential
     s.dtype = _abi.F32
-    assert _plan(h, m, s) == (4, 2, 1)  # packed fp32 pairs
+    assert _plan(h, m, s) == (2, 2, 1)  # packed fp32 pairs
     s = _sweep(n=8192)
     assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 8192) == 108  # one step: LDS halos fill the GPU
     assert _plan(h, m, s) == (8, 1, 1)

@@ -20,9 +20,21 @@ def test_help_lists_the_options():
     assert r.returncode == 0 and "--scaling" in r.stdout and "--dist-backend" in r.stdout
 
 
+def _committed_lines():
+    import glob
+
+    return sorted(glob.glob(f"{REPO}/profiles/r*/bench_line.json"))
+
+
 def test_committed_bench_line_keeps_the_contract():
-    """profiles/r1/bench_line.json has every key the driver's contract names."""
-    line = json.load(open(f"{REPO}/profiles/r1/bench_line.json"))
+    """profiles/r*/bench_line.json (one per round) has every key the driver's
+    contract names."""
+    assert _committed_lines()
+    for path in _committed_lines():
+        _check_line(json.load(open(path)))
+
+
+def _check_line(line):
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
                 "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert key in line, key
@@ -32,3 +44,16 @@ def test_committed_bench_line_keeps_the_contract():
     for key in ("value", "unit", "cores", "kind", "sample"):
         assert key in line["cpu_baseline"], key
     assert abs(line["roofline"]["frac"] - line["roofline"]["achieved"] / line["roofline"]["peak"]) < 1e-9
+
+
+def test_pmc_record_matches_the_layout():
+    """roofline.traffic comes from the PMC passes of the kernel the bench runs:
+    same dtype, chains, shape and lanes-per-chain layout, newest round first."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    rec, src = bench.pmc_record("f64", 65536, 4)
+    assert rec is not None and src.startswith("profiles/r") and "40, 4, true" in " ".join(rec["kernel"])
+    assert rec["hbm_bytes_per_launch"] > 0
+    assert bench.pmc_record("f64", 65536, 8) == (None, None)  # no PMC pass of that layout
+    assert bench.pmc_record("f64", 1000, 4) == (None, None)

@@ -72,6 +72,12 @@ def main():
         rec["effective_clock_GHz"] = rec["GRBM_GUI_ACTIVE"] / 8 / ns
     if "SQ_INSTS_VALU" in rec and "SQ_WAVES" in rec:
         rec["valu_instr_per_wave"] = rec["SQ_INSTS_VALU"] / rec["SQ_WAVES"]
+    if "SQ_INSTS_VALU" in rec and "effective_clock_GHz" in rec:
+        # VALU instructions issued per SIMD per cycle over the kernel (1 024
+        # SIMDs): a wave64 FP64 (or packed FP32) op holds its 16-lane SIMD for
+        # 4 cycles, so 0.25 is the FP64 / packed-FP32 pipe issuing every slot
+        cycles = rec["effective_clock_GHz"] * ns
+        rec["valu_issue_per_simd_cycle"] = rec["SQ_INSTS_VALU"] / (1024 * cycles)
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec))
