@@ -88,11 +88,10 @@ static bool l96_has(int D, int dtype, int lpc, int cpl) {
 //  1. the fewest lanes per chain whose halos go by DPP (LPC 1, 2, 4, 16) that
 //     still gives every SIMD one wave (kWaveLanes lanes), packed fp32 (CPL 2)
 //     first; more lanes only add halo work, fewer leave SIMDs idle.  With more
-//     components per lane than fit (packed fp32 20: the in-place RK4 state,
-//     l96_stage, in 256 VGPRs; fp64 16: spill-free two-wave occupancy) the
-//     next layout (LPC 2 -> 4, <= 4 waves).  d=40, 65 536 chains: packed fp32
-//     LPC 2 1.70 vs LPC 4 1.83 ms; fp64 LPC 2 only 1 % ahead of LPC 4 and
-//     then at 3.6x the HBM bytes (profiles/r2/lanes_inplace.txt);
+//     than 20 components per lane (the in-place RK4 state, l96_stage, no
+//     longer fits 256 VGPRs) the next layout (LPC 2 -> 4, <= 4 waves).
+//     d=40, 65 536 chains, LPC 2 vs 4 on the same box: packed fp32 1.75 vs
+//     1.85 ms, fp64 3.32 vs 3.37 ms (profiles/r2/lanes_scan_d40_r2k.txt);
 //  2. else any compiled layout reaching one wave (LPC 8: halos through LDS);
 //  3. else (an ensemble below one wave per SIMD, where the speculative sweep
 //     fills lanes with slots) the most DPP lanes per chain that keep >= 4
@@ -123,10 +122,9 @@ static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
     for (int i = 0; i < 4; ++i) {
       int l = dpp[i];
       if (!ok(l, c) || groups * l < kWaveLanes) continue;
-      // packed fp32 beyond 20 components per lane (the in-place RK4 state no
-      // longer fits 256 VGPRs), fp64 beyond 16 (two-wave occupancy would spill
-      // around every G): split the chain over twice the lanes
-      if (D / l > (c == 2 ? 20 : 16) && l <= 2 && ok(2 * l, c) && groups * 2 * l <= 4 * kWaveLanes) l *= 2;
+      // beyond 20 components per lane the in-place RK4 state (5 arrays) no
+      // longer fits 256 VGPRs: split the chain over twice the lanes
+      if (D / l > 20 && l <= 2 && ok(2 * l, c) && groups * 2 * l <= 4 * kWaveLanes) l *= 2;
       lpc = l;
       cpl = c;
       return;

@@ -139,9 +139,8 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
 // RK loop keeps 5 arrays of M values live (x, F, time-average, k-sum, stage;
 // l96_stage consumes each rate as it is computed), the proposal / accept stage
 // ~40 registers of addressing / RNG / loop state around it.  The target is
-// sized for 6 arrays: with 5, fp64 M = 20 fits two waves only by spilling
-// ~230 B per lane around every G evaluation (3.6x the compulsory HBM bytes of
-// the headline sweep, profiles/r2/pmc_l96_f64_lpc2_spill.json) for 1 % speed.
+// sized for 6 arrays (fp64 M = 20 then takes all 256 VGPRs FP64 operands can
+// address, i.e. two waves, without scratch).
 // (fp32 one chain per lane group: the compiler's SLP packing needs ~96; every
 // variant gets at least 104 registers, i.e. at most 4 waves, since the
 // proposal / accept stage spills below that: 20-56 B per lane at 5 waves for

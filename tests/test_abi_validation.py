@@ -162,12 +162,12 @@ def test_diagnostics_checks(h):
 
 
 def test_auto_layout(h):
-    """The layout the sweep picks by itself: fp64 d=40 -> 4 lanes per
+    """The layout the sweep picks by itself: fp64 d=40 -> 2 lanes per
     chain; fp32 -> two chains per lane group as f32x2, 2 lanes; d=256 -> 16 lanes."""
     m = _model()
-    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 65536) == 104
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 65536) == 102
     assert h.ipmc_auto_layout(C.byref(m), _abi.F32, 65536) == 202
-    assert h.ipmc_auto_lanes(C.byref(m), _abi.F64, 65536) == 4
+    assert h.ipmc_auto_lanes(C.byref(m), _abi.F64, 65536) == 2
     m = _model(dim=256, k=256, q=256)
     assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 131072) == 116
     assert h.ipmc_auto_layout(None, _abi.F64, 1) == 0
@@ -175,11 +175,12 @@ def test_auto_layout(h):
 
 # (dim, dtype, chains) -> cpl * 100 + lpc: the measured-fastest layout, or one
 # within 4 % of it, of profiles/r1/lanes_layout_rule.txt (d=40 at 32 768 and
-# 65 536 chains: profiles/r2/lanes_inplace.txt, after the in-place RK4 stages)
+# 65 536 chains: profiles/r2/lanes_inplace.txt, lanes_scan_d40_r2k.txt, after
+# the in-place RK4 stages)
 LAYOUT_TABLE = [
     (8, "f64", 16384, 104), (8, "f64", 65536, 101), (8, "f32", 16384, 104), (8, "f32", 65536, 202),
     (16, "f64", 16384, 104), (16, "f64", 65536, 101), (16, "f32", 16384, 104), (16, "f32", 65536, 202),
-    (40, "f64", 8192, 108), (40, "f64", 16384, 104), (40, "f64", 32768, 104), (40, "f64", 65536, 104),
+    (40, "f64", 8192, 108), (40, "f64", 16384, 104), (40, "f64", 32768, 102), (40, "f64", 65536, 102),
     (40, "f32", 8192, 108), (40, "f32", 16384, 104), (40, "f32", 32768, 204), (40, "f32", 65536, 202),
     (80, "f64", 16384, 104), (80, "f64", 65536, 104), (80, "f32", 16384, 216), (80, "f32", 65536, 204),
     # below one wave per SIMD (speculative sweeps): DPP halos (profiles/r1/l96_small_layouts.jsonl)
@@ -234,7 +235,7 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     another layout than ipmc_auto_layout's one-step pick)."""
     m = _model(dim=40, k=40, q=40)
     s = _sweep(n=65536)
-    assert _plan(h, m, s) == (4, 1, 1)  # headline: 4 lanes per chain, sequential
+    assert _plan(h, m, s) == (2, 1, 1)  # headline: 2 lanes per chain, sequential
     s.dtype = _abi.F32
     assert _plan(h, m, s) == (2, 2, 1)  # packed fp32 pairs
     s = _sweep(n=8192)
