@@ -198,7 +198,7 @@ void orc_l96ts_rhs_f64(int32_t arith, int32_t K, int32_t J, const double* x, con
 
 /* Rusanov pieces for the rusanov.py:112-170 known-answer tests. */
 double orc_rusanov_flux_f64(int32_t arith, double a, double b) {
-  return arith == IPMC_ARITH_FMA ? rus_flux_fm_f64(a, b, 0.25, -0.5) : rus_flux_f64(a, b);
+  return arith == IPMC_ARITH_FMA ? rus_flux_fm_f64(a, b, 0.25, -0.5, 0, 0.0) : rus_flux_f64(a, b);
 }
 void orc_rusanov_rate_f64(int32_t arith, int32_t N, const double* w, double dx, double* r) {
   rus_rate_f64(arith == IPMC_ARITH_FMA, N, w, -dx, 0.0, 0, r);

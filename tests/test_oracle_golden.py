@@ -366,3 +366,46 @@ def test_dense_prior_chain_matches_reference_sampler(orc, golden, case):
             samples[:, b - 1] = U
     np.testing.assert_array_equal(samples, golden[f"{key}_samples"])
     assert np.array_equal(acc, golden[f"{key}_accepts"])
+
+
+def _burgers_textbook(op, u):
+    """Viscous Burgers by the textbook form in numpy float64: SSPRK2 with
+    L(w) = -(F_{i+1/2} - F_{i-1/2})/dx + nu (w_{i+1} - 2 w_i + w_{i-1})/dx^2,
+    Rusanov F, outflow ghosts (rusanov.py:62-100), fixed dt, then the
+    Measurer windows (utilities.py:82-109)."""
+    left, right, jump = 1.0 + op.theta0[0] + u[0], op.theta0[1] + u[1], op.theta0[2] + u[2]
+    w = np.where(op.x < jump, left, right).astype(np.float64)
+    dx, nu, dt = op.dx, op.nu, op.dt
+
+    def rate(w):
+        a, b = w[:-1], w[1:]
+        F = 0.25 * (a * a + b * b) - 0.5 * np.maximum(np.abs(a), np.abs(b)) * (b - a)
+        r = np.zeros_like(w)
+        r[1:-1] = -(F[1:] - F[:-1]) / dx + nu * (w[2:] - 2.0 * w[1:-1] + w[:-2]) / dx**2
+        return r
+
+    for _ in range(op.n_steps):
+        ws = w + dt * rate(w)
+        ws[0], ws[-1] = ws[1], ws[-2]
+        ws = ws + dt * rate(ws)
+        w = 0.5 * (w + ws)
+        w[0], w[-1] = w[1], w[-2]
+    v = w[1:-1]
+    return np.array([op.meas_scale * np.trapz(v[lo:hi], dx=op.meas_dx) for lo, hi in zip(op.win_lo, op.win_hi)])
+
+
+@pytest.mark.parametrize("arith", ["fma", "reference"])
+def test_viscous_burgers_is_the_central_difference_scheme(orc, arith):
+    """The viscous extension (no reference exists): FMA arith folds nu/dx^2 into
+    the Rusanov flux's wave-speed term, REFERENCE arith adds the central
+    difference; both are the textbook scheme to rounding (1e-10 relative)."""
+    from ip_mcmc_amd import BurgersOperator
+
+    op = BurgersOperator(N=64, dt_mode="fixed", dt=2e-3, n_steps=300, nu=2e-3, arith=arith)
+    for u in ([0.0, 0.0, 0.0], [0.05, -0.1, 0.2], [-0.2, 0.1, -0.3]):
+        u = np.asarray(u)
+        g = orc.forward(op, u[None, :])[0]
+        want = _burgers_textbook(op, u)
+        assert np.allclose(g, want, rtol=1e-10, atol=1e-12), (arith, u, g, want)
+    inv = BurgersOperator(N=64, dt_mode="fixed", dt=2e-3, n_steps=300, nu=0.0, arith=arith)
+    assert not np.allclose(orc.forward(inv, u[None, :])[0], want, rtol=1e-6)  # the viscous term matters here
