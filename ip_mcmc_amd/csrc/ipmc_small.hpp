@@ -43,7 +43,10 @@ __device__ __forceinline__ void l63_forward(T sg, T rh, T bb, const T* __restric
     l63_rhs<T, FM>(sg, rh, bb, xs, k4);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const T a = ((k1[i] + (T)2 * k2[i]) + (T)2 * k3[i]) + k4[i];
+      // ((k1 + 2 k2) + 2 k3) + k4: 2k is exact, so FMA arith fuses the
+      // doublings (3 VALU ops instead of 5, the same bits as the oracle's form)
+      const T a = FM ? madd<true>((T)2, k3[i], madd<true>((T)2, k2[i], k1[i])) + k4[i]
+                     : ((k1[i] + (T)2 * k2[i]) + (T)2 * k3[i]) + k4[i];
       x[i] = madd<FM>(h6, a, x[i]);
     }
 #pragma unroll

@@ -409,3 +409,38 @@ def test_viscous_burgers_is_the_central_difference_scheme(orc, arith):
         assert np.allclose(g, want, rtol=1e-10, atol=1e-12), (arith, u, g, want)
     inv = BurgersOperator(N=64, dt_mode="fixed", dt=2e-3, n_steps=300, nu=0.0, arith=arith)
     assert not np.allclose(orc.forward(inv, u[None, :])[0], want, rtol=1e-6)  # the viscous term matters here
+
+
+def _l63_textbook(theta, x0, dt, n):
+    """Classical RK4 Lorenz-63 in numpy float64, G = time averages of
+    (x, y, z, x^2, y^2, z^2) over the n post-step states."""
+    sg, rh, bb = theta
+
+    def f(s):
+        return np.array([sg * (s[1] - s[0]), s[0] * (rh - s[2]) - s[1], s[0] * s[1] - bb * s[2]])
+
+    x = np.asarray(x0, dtype=np.float64).copy()
+    ob = np.zeros(6)
+    for _ in range(n):
+        k1 = f(x)
+        k2 = f(x + 0.5 * dt * k1)
+        k3 = f(x + 0.5 * dt * k2)
+        k4 = f(x + dt * k3)
+        x = x + dt / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
+        ob += np.concatenate([x, x * x])
+    return ob / n
+
+
+@pytest.mark.parametrize("arith", ["fma", "reference"])
+def test_lorenz63_oracle_is_textbook_rk4(orc, arith):
+    """Lorenz-63 has no reference implementation: the oracle's G
+    (both arithmetic modes) is classical RK4 to rounding over a horizon short
+    enough that the chaos does not amplify it (1e-11 relative)."""
+    from ip_mcmc_amd import Lorenz63Operator
+
+    op = Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=150, arith=arith)
+    for u in ([0.0, 0.0, 0.0], [0.5, -1.0, 0.1], [-1.0, 2.0, -0.2]):
+        u = np.asarray(u)
+        g = orc.forward(op, u[None, :])[0]
+        want = _l63_textbook(op.theta0 + u, op.x0, op.dt, op.n_steps)
+        assert np.allclose(g, want, rtol=1e-11, atol=1e-11), (arith, u, g - want)
