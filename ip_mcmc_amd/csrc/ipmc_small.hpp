@@ -212,10 +212,23 @@ __device__ __forceinline__ T lin_potential_staged(const T* As, const T* ys, cons
   return (T)0.5 * s;
 }
 
+// Linear G: a round is a few FMAs of Φ, so its latency is the Philox /
+// Box–Muller draws of the slots' steps.  The draws do not depend on the chain
+// state, so the linear sweep computes them ahead, kPreFactor*S steps at a time
+// spread over the group's lanes (w = sqrt(C)·ξ or L·ξ, and log r, in the
+// sequential kernel's operations), into LDS; a round then reads them and only
+// forms v, Φ(v) and the comparison -- the same bits, a much shorter round.
+constexpr int kPreFactor = 4;
+constexpr int kPreLds = kPreFactor * kSpecBlock;  // steps per block (all groups)
+
 template <typename T, int MODEL, bool FM, int S>
 __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model m, const ipmc_sweep s) {
+  constexpr bool PRE = (MODEL == IPMC_MODEL_LINEAR);
+  constexpr int C = kPreFactor * S;  // steps of draws a group holds
   __shared__ T vpark[kSpecKMax * kSpecBlock];
   __shared__ T lin_c[MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1];
+  __shared__ T pre_w[PRE ? kPreLds * kSpecKMax : 1];    // [group][step in chunk][j]
+  __shared__ double pre_lr[PRE ? kPreLds : 1];           // [group][step in chunk]: log r
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int sub = t & (S - 1);
@@ -266,9 +279,62 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   T phu = phi[chain];
   int64_t nacc = 0, ncalls = 0;
   int64_t st = 0;
+  // PRE: draws of steps [pbase, pbase + C) of this group, in pre_w / pre_lr
+  const int grp = (t - sub) / S;  // this group's index in the block
+  T* gw = pre_w + (PRE ? grp * C * kSpecKMax : 0);
+  double* glr = pre_lr + (PRE ? grp * C : 0);
+  int64_t pbase = 0, pend = 0;
+  // w_j of step tt (sqrt(C_jj)·ξ_j or Σ_{i<=j} L_ji ξ_i), in the sequential kernel's order
+  auto draw_w = [&](uint64_t step, T (&w)[kSpecKMax]) {
+    double z0 = 0.0, z1 = 0.0;
+    T xi[kSpecKMax];
+    if (chol) {
+#pragma unroll
+      for (int j = 0; j < kSpecKMax; j += 2) {
+        if (j < k) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+        xi[j] = (T)z0;
+        xi[j + 1] = (T)z1;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kSpecKMax; ++j) {
+      w[j] = (T)0;
+      if (j < k) {
+        if (chol) {
+#pragma unroll
+          for (int i = 0; i <= j; ++i) w[j] = w[j] + xi[i] * chol[j * k + i];
+        } else {
+          if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+          w[j] = sqr[j] * (T)((j & 1) ? z1 : z0);
+        }
+      }
+    }
+  };
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + sub;
+    if constexpr (PRE) {
+      // refill when this round's slots reach past the held draws (uniform per group)
+      if (st + S > pend && pend < s.n_steps) {
+        pbase = st;
+        pend = st + C;
+        wave_sync_lds();  // the previous chunk's reads are done
+#pragma unroll
+        for (int r = 0; r < kPreFactor; ++r) {  // independent draws: the compiler interleaves them
+          const int i = sub + r * S;
+          const int64_t ti = pbase + i;
+          if (ti < s.n_steps) {
+            const uint64_t step = s.step0 + (uint64_t)ti;
+            T w[kSpecKMax];
+            draw_w(step, w);
+#pragma unroll
+            for (int j = 0; j < kSpecKMax; ++j) gw[i * kSpecKMax + j] = w[j];
+            glr[i] = det_log(accept_uniform(s.seed, gid, step));
+          }
+        }
+        wave_sync_lds();
+      }
+    }
     bool ok = false, acc = false;
     T phv = (T)0;
     if (sub < left) {
@@ -278,7 +344,19 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       double z0 = 0.0, z1 = 0.0;
       ok = true;
       T xi[kSpecKMax];
-      if (chol) {
+      if (PRE) {
+        const int pi = (int)(tt - pbase);
+#pragma unroll
+        for (int j = 0; j < kSpecKMax; ++j) {
+          if (j < k) {
+            const T vj = propose_one<T>(rw, ur[j], gw[pi * kSpecKMax + j], cs, bs);
+            v[j * kSpecBlock] = vj;
+            const T tb = vj + offr[j];
+            if (lo && !(lor[j] < tb)) ok = false;
+            if (hi && !(tb < hir[j])) ok = false;
+          }
+        }
+      } else if (chol) {
 #pragma unroll
         for (int j = 0; j < kSpecKMax; j += 2) {
           if (j < k) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
@@ -288,7 +366,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       }
 #pragma unroll
       for (int j = 0; j < kSpecKMax; ++j) {
-        if (j < k) {
+        if (!PRE && j < k) {
           T w;
           if (chol) {  // non-diagonal prior: chol_propose's order
             w = (T)0;
@@ -324,7 +402,8 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
           }
           phv = phv + (T)0.5 * r2;
         }
-        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+        if constexpr (PRE) acc = (double)(phu - phv) > glr[tt - pbase];  // pcn_accept with its log r
+        else acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
       }
     }
     wave_sync_lds();
