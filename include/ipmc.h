@@ -7,6 +7,7 @@
  *   reference (ochsnerd/ip_mcmc, pure Python, one chain)      this ABI (many chains, device)
  *   ------------------------------------------------------    -----------------------------------
  *   MCMCSampler.run / _step           sampler.py:12-41        ipmc_pcn_sweep   (n_steps steps/launch)
+ *   MCMCSampler.run sampling loop     sampler.py:23-28        ipmc_pcn_run     (one launch per sample, in C)
  *   ConstSteppCNProposer.__call__     proposer.py:81-82       ipmc_pcn_sweep   (proposal stage)
  *   VarSteppCNProposer.__call__       proposer.py:110-115     ipmc_pcn_sweep   (host passes beta per launch)
  *   ProbabilisticAccepter.__call__    accepter.py:59-62       ipmc_pcn_sweep   (accept stage)
@@ -53,7 +54,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 7
+#define IPMC_ABI_VERSION 8
 
 typedef enum {
   IPMC_OK = 0,
@@ -164,6 +165,17 @@ typedef struct ipmc_sweep {
 /* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */
 int ipmc_pcn_sweep(const ipmc_model* model, const ipmc_sweep* sweep, void* stream);
 
+/* MCMCSampler.run's sampling loop (sampler.py:23-28) in one call: n_blocks
+   consecutive ipmc_pcn_sweep launches of block_steps steps each, block b
+   starting at global step sweep->step0 + b*block_steps (sweep->n_steps is
+   ignored) and, if sweep->sample_out is set, writing u after its last step to
+   sample_out + b*sample_block_stride elements (rows still sweep->sample_stride
+   apart: samples [n_chains, n_samples, k] take sample_block_stride = k);
+   beta_schedule, if set, holds all n_blocks*block_steps steps; sum_u / sum_u2
+   accumulate over every step.  The same results as the n_blocks calls, without
+   a host round trip per sample (config 1: 5 000 launches of 200 steps). */
+int ipmc_pcn_run(const ipmc_model* model, const ipmc_sweep* sweep, int64_t n_blocks, int64_t block_steps,
+                 int64_t sample_block_stride, void* stream);
 /* sweep->phi[c] = the accept potential of sweep->u[c] for every chain: Φ(u), or
    I(u) = Φ(u) + ½Σ(reg_scale_i u_i)² when sweep->reg_scale is set (call before the first sweep). */
 int ipmc_init_phi(const ipmc_model* model, const ipmc_sweep* sweep, void* stream);

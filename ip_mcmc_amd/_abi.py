@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -98,6 +98,8 @@ class IpmcPlan(C.Structure):
 # Exported symbols of libipmc.so and their ctypes signatures (include/ipmc.h).
 SIGNATURES = {
     "ipmc_pcn_sweep": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.c_void_p]),
+    "ipmc_pcn_run": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.c_int64, C.c_int64, C.c_int64,
+                               C.c_void_p]),
     "ipmc_init_phi": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.c_void_p]),
     "ipmc_potential": (
         C.c_int,

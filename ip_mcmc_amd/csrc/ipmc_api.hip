@@ -454,6 +454,28 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   return fail(IPMC_ERR_UNSUPPORTED, "unknown model kind");
 }
 
+int ipmc_pcn_run(const ipmc_model* m, const ipmc_sweep* s, int64_t n_blocks, int64_t block_steps,
+                 int64_t sample_block_stride, void* stream) {
+  if (!s) return fail(IPMC_ERR_INVALID, "sweep is NULL");
+  if (n_blocks < 0 || block_steps < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (block_steps > 0x7fffffff) return fail(IPMC_ERR_INVALID, "block_steps must be < 2^31");
+  if (n_blocks > 0 && (uint64_t)block_steps > 0 &&
+      (uint64_t)n_blocks > (kHostStepBase - s->step0) / (uint64_t)block_steps)
+    return fail(IPMC_ERR_INVALID, "pCN steps must stay below 2^63 (the host-draw range)");
+  if (s->sample_out && sample_block_stride < 0) return fail(IPMC_ERR_INVALID, "negative sample_block_stride");
+  const size_t es = s->dtype == IPMC_F64 ? 8 : 4;
+  ipmc_sweep b = *s;
+  b.n_steps = block_steps;
+  for (int64_t i = 0; i < n_blocks; ++i) {  // sampler.py:23-28, one launch per block
+    b.step0 = s->step0 + (uint64_t)(i * block_steps);
+    if (s->sample_out) b.sample_out = (char*)s->sample_out + (size_t)(i * sample_block_stride) * es;
+    if (s->beta_schedule) b.beta_schedule = s->beta_schedule + 2 * i * block_steps;
+    const int rc = ipmc_pcn_sweep(m, &b, stream);
+    if (rc) return rc;
+  }
+  return IPMC_OK;
+}
+
 int ipmc_init_phi(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   if (!s) return fail(IPMC_ERR_INVALID, "sweep is NULL");
   int rc = dispatch_eval(m, s->dtype, s->n_chains, s->u, s->y, s->gamma_inv, s->phi, true, stream);

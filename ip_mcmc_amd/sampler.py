@@ -273,6 +273,30 @@ class MCMCSampler:
             step += n
             prop_i += n
 
+        def launch_blocks(nb, block, first_view, sums):
+            """nb blocks of `block` steps, block b's end state into first_view's
+            sample slot + b (ipmc_pcn_run: the sampling loop without a host
+            round trip per sample)."""
+            nonlocal step, prop_i
+            sched = None
+            if not const_beta:
+                sched = torch.as_tensor(plan.proposer.beta_schedule(prop_i, nb * block)).to(device)
+                keep_alive.append(sched)
+                sw.beta, sw.contraction = 0.0, 1.0
+            sw.beta_schedule = dev.ptr(sched)
+            sw.step0 = step
+            sw.n_steps = block
+            if first_view is not None:
+                sw.sample_out = first_view.data_ptr()
+                sw.sample_stride = first_view.stride(0)
+            else:
+                sw.sample_out = None
+                sw.sample_stride = 0
+            sw.sum_u, sw.sum_u2 = (None, None) if sums is None else (sums[0].data_ptr(), sums[1].data_ptr())
+            call("ipmc_pcn_run", C.byref(model), C.byref(sw), nb, block, k, stream)
+            step += nb * block
+            prop_i += nb * block
+
         t0 = time.perf_counter()
         spl = _steps_per_launch(model, n_chains)
         n_burn = max(0, burn_in - sample_interval)  # sampler.py:18
@@ -299,7 +323,18 @@ class MCMCSampler:
                 torch.zeros((n_chains, k), dtype=torch.float64, device=device),
                 torch.zeros((n_chains, k), dtype=torch.float64, device=device),
             )
-        for i in range(n_samples):  # sampler.py:23-28
+        # one launch per sample: the whole loop (up to the next streaming flush)
+        # in one ipmc_pcn_run call; consecutive sample slots are k elements apart
+        blockwise = (not self.verbose) and 0 < sample_interval <= spl
+        i = 0
+        while blockwise and i < n_samples:  # sampler.py:23-28
+            slot = i % buf_len  # 0: segments end where the staging buffer is full
+            nb = min(n_samples - i, buf_len - slot)
+            launch_blocks(nb, sample_interval, None if samples is None else samples[:, slot, :], sums)
+            if sink is not None:
+                samples = writer.flush(i - slot, slot + nb)
+            i += nb
+        for i in range(0 if not blockwise else n_samples, n_samples):  # sampler.py:23-28
             if self.verbose:
                 print(f"Sampling {i + 1}/{n_samples}")
             slot = i % buf_len

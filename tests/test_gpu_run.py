@@ -1,0 +1,79 @@
+"""ipmc_pcn_run (MCMCSampler.run's sampling loop in one C call) gives the bits
+of the per-sample launches it replaces: samples, moments, accept counts and
+the chain state, for constant and scheduled step sizes and small (speculative)
+and large ensembles."""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return torch.device("cuda", 0)
+
+
+def _sampler(op, y, gamma, var_step, chains_seed=5):
+    from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             MCMCSampler, PhiloxRNG, VarSteppCNProposer, pCNAccepter)
+
+    prior = GaussianDistribution(np.zeros(op.k), np.eye(op.k))
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(op.q), gamma**2 * np.eye(op.q)))
+    prop = VarSteppCNProposer(lambda i: 0.1 + 0.4 / (1 + i), prior) if var_step else ConstSteppCNProposer(0.3, prior)
+    acc = CountedAccepter(pCNAccepter(pot))
+    return MCMCSampler(prop, acc, PhiloxRNG(chains_seed)), acc
+
+
+def _run(op, y, gamma, var_step, u0, keep, verbose, **kw):
+    s, acc = _sampler(op, y, gamma, var_step)
+    s.verbose = verbose  # verbose keeps the per-sample launch loop (it prints every sample)
+    with contextlib.redirect_stdout(io.StringIO()):
+        out = s.run(u0, keep=keep, **kw)
+    return out, np.asarray(acc.accepts), s.state.u
+
+
+@pytest.mark.parametrize("case", ["linear1", "linear4096", "l96", "l96_var"])
+@pytest.mark.parametrize("keep", ["samples", "moments"])
+def test_pcn_run_equals_per_sample_launches(dev, case, keep):
+    from ip_mcmc_amd import LinearOperator, Lorenz96Operator
+
+    rng = np.random.default_rng(2)
+    if case.startswith("linear"):
+        op = LinearOperator(rng.normal(size=(3, 4)))
+        y, gamma = rng.normal(size=3), 0.5
+        n = 1 if case == "linear1" else 4096
+    else:
+        op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=50)
+        y, gamma = op(np.zeros(8)) + 0.1 * rng.normal(size=8), 0.2
+        n = 300
+    u0 = 0.1 * rng.normal(size=(n, op.k))
+    kw = dict(n_samples=37, burn_in=25, sample_interval=6)
+    a = _run(op, y, gamma, case.endswith("var"), u0, keep, False, **kw)
+    b = _run(op, y, gamma, case.endswith("var"), u0, keep, True, **kw)
+    if keep == "samples":
+        assert a[0].shape == (n, 37, op.k) and np.array_equal(a[0], b[0])
+    else:
+        assert np.array_equal(a[0]["sum_u"], b[0]["sum_u"]) and np.array_equal(a[0]["sum_u2"], b[0]["sum_u2"])
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[1].sum() > 0
+
+
+def test_pcn_run_streams_to_a_file(dev, tmp_path):
+    """run(sample_file=...) through ipmc_pcn_run, flushing every 5 samples,
+    equals the in-memory run."""
+    from ip_mcmc_amd import LinearOperator
+
+    rng = np.random.default_rng(3)
+    op = LinearOperator(rng.normal(size=(2, 4)))
+    y = rng.normal(size=2)
+    u0 = 0.1 * rng.normal(size=(64, 4))
+    s1, _ = _sampler(op, y, 0.5, False)
+    mem = s1.run(u0, n_samples=23, burn_in=10, sample_interval=3)
+    s2, _ = _sampler(op, y, 0.5, False)
+    f = s2.run(u0, n_samples=23, burn_in=10, sample_interval=3, sample_file=str(tmp_path / "s.npy"), flush_every=5)
+    assert np.array_equal(np.asarray(f), mem)
