@@ -286,3 +286,23 @@ def test_unsupported_layout_sets_the_error_message(h):
     s = _sweep()
     s.lanes_per_chain = 3
     _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_UNSUPPORTED, "lanes_per_chain=3")
+
+
+def test_pcn_run_validation(h):
+    """ipmc_pcn_run checks its block arithmetic before launching anything, and
+    every block goes through ipmc_pcn_sweep's own checks."""
+    m = C.byref(_model())
+    _status(h, h.ipmc_pcn_run(m, None, 1, 1, 40, None), _abi.ERR_INVALID, "sweep is NULL")
+    _status(h, h.ipmc_pcn_run(m, C.byref(_sweep()), -1, 1, 40, None), _abi.ERR_INVALID, "negative count")
+    _status(h, h.ipmc_pcn_run(m, C.byref(_sweep()), 1, -1, 40, None), _abi.ERR_INVALID, "negative count")
+    _status(h, h.ipmc_pcn_run(m, C.byref(_sweep()), 1, 1 << 31, 40, None), _abi.ERR_INVALID, "< 2^31")
+    s = _sweep()
+    s.step0 = (1 << 62)
+    _status(h, h.ipmc_pcn_run(m, C.byref(s), 1 << 43, 1 << 20, 40, None), _abi.ERR_INVALID, "below 2^63")
+    s = _sweep()
+    s.sample_out, s.sample_stride = DUMMY, 40
+    _status(h, h.ipmc_pcn_run(m, C.byref(s), 2, 3, -1, None), _abi.ERR_INVALID, "sample_block_stride")
+    s = _sweep()
+    s.beta = 2.0  # the per-block checks of ipmc_pcn_sweep
+    _status(h, h.ipmc_pcn_run(m, C.byref(s), 2, 3, 40, None), _abi.ERR_INVALID, "beta has to be in")
+    assert h.ipmc_pcn_run(m, C.byref(_sweep()), 0, 5, 40, None) == _abi.OK  # no block: nothing to do
