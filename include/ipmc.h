@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 8
+#define IPMC_ABI_VERSION 9
 
 typedef enum {
   IPMC_OK = 0,
@@ -160,6 +160,13 @@ typedef struct ipmc_sweep {
   const void* prior_chol;   /* optional [k, k] row-major lower Cholesky factor L of a NON-diagonal prior covariance
                                (GaussianDistribution.L): w_j = sum_{i<=j} L[j][i] xi_i in ascending i, overriding
                                prior_sqrt (which may then be NULL); proposer.py:81-82's w ~ N(0, C) */
+  int64_t sample_every;     /* 0: sample_out receives u after the last step of the launch (above).  > 0: samples
+                               inside the launch, MCMCSampler.run's recording (sampler.py:23-28): u after every
+                               step j (0-based in this launch) with (j+1) % sample_every == 0 goes to
+                               sample_out + ((j+1)/sample_every - 1)*sample_step_stride (+ chain*sample_stride);
+                               nothing else is written.  One launch then covers many samples and the speculative
+                               sweeps run across sample boundaries. */
+  int64_t sample_step_stride; /* elements between consecutive samples of one chain (>= k when sample_every > 0) */
 } ipmc_sweep;
 
 /* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */
@@ -173,7 +180,8 @@ int ipmc_pcn_sweep(const ipmc_model* model, const ipmc_sweep* sweep, void* strea
    apart: samples [n_chains, n_samples, k] take sample_block_stride = k);
    beta_schedule, if set, holds all n_blocks*block_steps steps; sum_u / sum_u2
    accumulate over every step.  The same results as the n_blocks calls, without
-   a host round trip per sample (config 1: 5 000 launches of 200 steps). */
+   a host round trip per sample.  With sweep->sample_every > 0 each block
+   records its in-launch samples from sample_out + b*sample_block_stride. */
 int ipmc_pcn_run(const ipmc_model* model, const ipmc_sweep* sweep, int64_t n_blocks, int64_t block_steps,
                  int64_t sample_block_stride, void* stream);
 /* sweep->phi[c] = the accept potential of sweep->u[c] for every chain: Φ(u), or

@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -83,6 +83,8 @@ class IpmcSweep(C.Structure):
         ("sum_u", C.c_void_p),
         ("sum_u2", C.c_void_p),
         ("prior_chol", C.c_void_p),
+        ("sample_every", C.c_int64),
+        ("sample_step_stride", C.c_int64),
     ]
 
 

@@ -412,8 +412,12 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
   if (s->n_steps > 0x7fffffff) return fail(IPMC_ERR_INVALID, "n_steps per launch must be < 2^31");
   if (s->step0 > kHostStepBase - (uint64_t)s->n_steps)
     return fail(IPMC_ERR_INVALID, "pCN steps must stay below 2^63 (the host-draw range)");
+  if (s->sample_every < 0 || s->sample_every > 0x7fffffff)
+    return fail(IPMC_ERR_INVALID, "sample_every must be in [0, 2^31)");
+  if (s->sample_every > 0 && (!s->sample_out || s->sample_step_stride < m->k || s->sample_stride < m->k))
+    return fail(IPMC_ERR_INVALID, "sample_every needs sample_out, sample_stride >= k and sample_step_stride >= k");
   if (s->n_chains == 0 || s->n_steps == 0) {
-    if (s->n_chains > 0 && s->sample_out) {
+    if (s->n_chains > 0 && s->sample_out && s->sample_every == 0) {
       // no step: the sample is the current state
       const size_t es = s->dtype == IPMC_F64 ? 8 : 4;
       hipStream_t st = (hipStream_t)stream;

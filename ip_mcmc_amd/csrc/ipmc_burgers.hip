@@ -319,6 +319,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
   T phu = phi[chain];
   const unsigned long long gmask = (G >= 64) ? ~0ull : ((1ull << G) - 1);
   int nacc = 0, ncalls = 0;
+  SampleClock clk(s);
   int64_t st = 0;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
@@ -402,6 +403,16 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
         }
       }
     }
+    if (s.sample_every > 0 && r == 0) {
+      // the samples among the `used` steps: the state after step st+q
+      while (clk.next < st + used) {
+        const int q = (int)(clk.next - st);
+        const int64_t sl = clk.take(clk.next);
+        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) so[j] = (q == first) ? vf[j] : ur[j];
+      }
+    }
     if (first < S) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) ur[j] = vf[j];
@@ -416,7 +427,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
     if (s.calls) s.calls[chain] += ncalls;
 #pragma unroll
     for (int j = 0; j < 3; ++j) u[j] = ur[j];
-    if (s.sample_out) {
+    if (s.sample_out && s.sample_every == 0) {
       T* so = (T*)s.sample_out + chain * s.sample_stride;
 #pragma unroll
       for (int j = 0; j < 3; ++j) so[j] = ur[j];

@@ -236,13 +236,19 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
         if (su2) su2[j] += ud * ud;
       }
     }
+    const int64_t sl = sample_slot(s, st);
+    if (sl >= 0) {
+      T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) so[j] = u[j];
+    }
   }
   if (sub == 0) {
     phi[chain] = phu;
     if (s.accepts) s.accepts[chain] += nacc;
     if (s.calls) s.calls[chain] += ncalls;
   }
-  if (s.sample_out) {
+  if (s.sample_out && s.sample_every == 0) {
     T* so = (T*)s.sample_out + chain * s.sample_stride + c0;
 #pragma unroll
     for (int j = 0; j < M; ++j) so[j] = u[j];
@@ -287,6 +293,7 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
   const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
   const unsigned long long gmask = (G >= 64) ? ~0ull : ((1ull << G) - 1);
   int nacc = 0, ncalls = 0;
+  SampleClock clk(s);
   int64_t st = 0;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
@@ -360,6 +367,16 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
         }
       }
     }
+    if (s.sample_every > 0 && slot == 0) {
+      // the samples among the `used` steps: the state after step st+q
+      while (clk.next < st + used) {
+        const int q = (int)(clk.next - st);
+        const int64_t sl = clk.take(clk.next);
+        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) so[j] = (q == first) ? vpark[j][win] : ur[j];
+      }
+    }
     if (first < S) {
 #pragma unroll
       for (int j = 0; j < M; ++j) ur[j] = vpark[j][win];
@@ -378,7 +395,7 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
       if (s.accepts) s.accepts[chain] += nacc;
       if (s.calls) s.calls[chain] += ncalls;
     }
-    if (s.sample_out) {
+    if (s.sample_out && s.sample_every == 0) {
       T* so = (T*)s.sample_out + chain * s.sample_stride + c0;
 #pragma unroll
       for (int j = 0; j < M; ++j) so[j] = ur[j];
@@ -486,6 +503,17 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
         }
       }
     }
+    const int64_t sl = sample_slot(s, st);
+    if (sl >= 0) {
+      float* so = (float*)s.sample_out + ca * s.sample_stride + sl * s.sample_step_stride + c0;
+#pragma unroll
+      for (int j = 0; j < M; ++j) so[j] = ua[j];
+      if (has_b) {
+        float* sb = (float*)s.sample_out + cb * s.sample_stride + sl * s.sample_step_stride + c0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) sb[j] = ub[j];
+      }
+    }
   }
   if (sub == 0) {
     phi[ca] = pa;
@@ -497,7 +525,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
       if (s.calls) s.calls[cb] += kb;
     }
   }
-  if (s.sample_out) {
+  if (s.sample_out && s.sample_every == 0) {
     float* so = (float*)s.sample_out + ca * s.sample_stride + c0;
 #pragma unroll
     for (int j = 0; j < M; ++j) so[j] = ua[j];

@@ -303,6 +303,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
   T* phi = (T*)s.phi;
   T phu = phi[chain];
   int nacc = 0, ncalls = 0;
+  SampleClock clk(s);
   int64_t st = 0;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
@@ -358,6 +359,16 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
         }
       }
     }
+    if (s.sample_every > 0 && r == 0) {
+      // the samples among the `used` steps: the state after step st+qq
+      while (clk.next < st + used) {
+        const int qq = (int)(clk.next - st);
+        const int64_t sl = clk.take(clk.next);
+        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) so[j] = (qq == first) ? vf[j] : ur[j];
+      }
+    }
     if (first < S) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) ur[j] = vf[j];
@@ -372,7 +383,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
     if (s.calls) s.calls[chain] += ncalls;
 #pragma unroll
     for (int j = 0; j < 3; ++j) u[j] = ur[j];
-    if (s.sample_out) {
+    if (s.sample_out && s.sample_every == 0) {
       T* so = (T*)s.sample_out + chain * s.sample_stride;
 #pragma unroll
       for (int j = 0; j < 3; ++j) so[j] = ur[j];

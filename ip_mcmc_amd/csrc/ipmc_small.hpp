@@ -169,11 +169,16 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
         if (s.sum_u2) s.sum_u2[chain * k + j] += ud * ud;
       }
     }
+    const int64_t sl = sample_slot(s, st);
+    if (sl >= 0) {
+      T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+      for (int j = 0; j < k; ++j) so[j] = u[j];
+    }
   }
   phi[chain] = phu;
   if (s.accepts) s.accepts[chain] += nacc;
   if (s.calls) s.calls[chain] += ncalls;
-  if (s.sample_out) {
+  if (s.sample_out && s.sample_every == 0) {
     T* so = (T*)s.sample_out + chain * s.sample_stride;
     for (int j = 0; j < k; ++j) so[j] = u[j];
   }
@@ -278,6 +283,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   }
   T phu = phi[chain];
   int64_t nacc = 0, ncalls = 0;
+  SampleClock clk(s);
   int64_t st = 0;
   // PRE: draws of steps [pbase, pbase + C) of this group, in pre_w / pre_lr
   const int grp = (t - sub) / S;  // this group's index in the block
@@ -427,6 +433,17 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
         }
       }
     }
+    if (s.sample_every > 0 && sub == 0) {
+      // the samples among the `used` steps: the state after step st+q
+      while (clk.next < st + used) {
+        const int q = (int)(clk.next - st);
+        const int64_t sl = clk.take(clk.next);
+        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+#pragma unroll
+        for (int j = 0; j < kSpecKMax; ++j)
+          if (j < k) so[j] = (q == first) ? vgroup[j * kSpecBlock + first] : ur[j];
+      }
+    }
     if (first < S) {
 #pragma unroll
       for (int j = 0; j < kSpecKMax; ++j)
@@ -444,7 +461,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
 #pragma unroll
     for (int j = 0; j < kSpecKMax; ++j)
       if (j < k) u[j] = ur[j];
-    if (s.sample_out) {
+    if (s.sample_out && s.sample_every == 0) {
       T* so = (T*)s.sample_out + chain * s.sample_stride;
 #pragma unroll
       for (int j = 0; j < kSpecKMax; ++j)

@@ -153,6 +153,29 @@ __device__ __forceinline__ bool box_valid(const ipmc_sweep& s, int c0, const T (
   return group_all<LPC>(ok, lane);
 }
 
+// In-launch recording (ipmc_sweep.sample_every > 0, sampler.py:23-28): u
+// after step j (0-based in this launch) is sample (j+1)/every - 1 when
+// (j+1) % every == 0.
+// Sequential sweeps: from the (wave-uniform) step counter after G -- nothing
+// extra is live across G, whose RK loop may hold every register (a clock
+// carried across G changed the packed M = 20 kernel's register assignment).
+__device__ __forceinline__ int64_t sample_slot(const ipmc_sweep& s, int64_t j) {
+  return (s.sample_every > 0 && (j + 1) % s.sample_every == 0) ? (j + 1) / s.sample_every - 1 : -1;
+}
+// Speculative sweeps (several steps per round): tracked incrementally by the
+// recording lane -- `next` is the next such j -- so no step pays a division.
+struct SampleClock {
+  int64_t next, slot, every;
+  __device__ explicit SampleClock(const ipmc_sweep& s)
+      : next(s.sample_every > 0 ? s.sample_every - 1 : INT64_MAX), slot(0), every(s.sample_every) {}
+  // the state after step j is a sample: its slot (advancing the clock), else -1
+  __device__ __forceinline__ int64_t take(int64_t j) {
+    if (j != next) return -1;
+    next += every;
+    return slot++;
+  }
+};
+
 // accept iff Φ(u) − Φ(v) > log r   ⇔ exp(Φ(u) − Φ(v)) > r   (accepter.py:62, 121-122)
 template <typename T>
 __device__ __forceinline__ bool pcn_accept(T phu, T phv, uint64_t seed, uint64_t gid, uint64_t step) {

@@ -262,6 +262,7 @@ class MCMCSampler:
                 sw.beta, sw.contraction = 0.0, 1.0
             sw.step0 = step
             sw.n_steps = n
+            sw.sample_every = 0
             if sample_view is not None:
                 sw.sample_out = sample_view.data_ptr()
                 sw.sample_stride = sample_view.stride(0)
@@ -273,29 +274,39 @@ class MCMCSampler:
             step += n
             prop_i += n
 
-        def launch_blocks(nb, block, first_view, sums):
-            """nb blocks of `block` steps, block b's end state into first_view's
-            sample slot + b (ipmc_pcn_run: the sampling loop without a host
-            round trip per sample)."""
+        def launch_blocks(nb, interval, first_view, sums):
+            """nb samples `interval` steps apart, sample i into first_view's slot
+            + i: launches of up to `spl` steps that record their samples inside
+            the kernel (ipmc_sweep.sample_every), issued by ipmc_pcn_run -- no
+            host round trip per sample, and the speculative sweeps of small
+            ensembles run across sample boundaries."""
             nonlocal step, prop_i
+            per = max(1, spl // interval)  # samples per launch
             sched = None
             if not const_beta:
-                sched = torch.as_tensor(plan.proposer.beta_schedule(prop_i, nb * block)).to(device)
+                sched = torch.as_tensor(plan.proposer.beta_schedule(prop_i, nb * interval)).to(device)
                 keep_alive.append(sched)
                 sw.beta, sw.contraction = 0.0, 1.0
-            sw.beta_schedule = dev.ptr(sched)
-            sw.step0 = step
-            sw.n_steps = block
-            if first_view is not None:
-                sw.sample_out = first_view.data_ptr()
-                sw.sample_stride = first_view.stride(0)
-            else:
-                sw.sample_out = None
-                sw.sample_stride = 0
             sw.sum_u, sw.sum_u2 = (None, None) if sums is None else (sums[0].data_ptr(), sums[1].data_ptr())
-            call("ipmc_pcn_run", C.byref(model), C.byref(sw), nb, block, k, stream)
-            step += nb * block
-            prop_i += nb * block
+            sw.sample_every = interval if first_view is not None else 0
+            sw.sample_step_stride = k
+            done = 0
+            for n_launch, n_per in ((nb // per, per), (1 if nb % per else 0, nb % per)):
+                if n_launch == 0:
+                    continue
+                sw.step0 = step
+                sw.beta_schedule = 0 if sched is None else sched.data_ptr() + 16 * done * interval
+                if first_view is not None:
+                    sw.sample_out = first_view.data_ptr() + first_view.element_size() * done * k
+                    sw.sample_stride = first_view.stride(0)
+                else:
+                    sw.sample_out = None
+                    sw.sample_stride = 0
+                call("ipmc_pcn_run", C.byref(model), C.byref(sw), n_launch, n_per * interval, n_per * k, stream)
+                done += n_launch * n_per
+                step += n_launch * n_per * interval
+            prop_i += nb * interval
+            sw.sample_every = 0
 
         t0 = time.perf_counter()
         spl = _steps_per_launch(model, n_chains)

@@ -90,6 +90,8 @@ int orc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, int32_t n_threads) {
   if (st) return st;
   if (!s || !s->u || !s->phi || !s->y || !s->gamma_inv || (!s->prior_sqrt && !s->prior_chol)) return IPMC_ERR_INVALID;
   if (s->proposal == IPMC_PROPOSAL_PCN && !(s->beta >= 0.0 && s->beta <= 1.0)) return IPMC_ERR_INVALID;
+  if (s->sample_every < 0 || (s->sample_every > 0 && (!s->sample_out || s->sample_step_stride < m->k)))
+    return IPMC_ERR_INVALID;
   const int64_t C = s->n_chains;
   if (n_threads < 1) n_threads = 1;
 #pragma omp parallel for num_threads(n_threads) schedule(static)

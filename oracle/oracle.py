@@ -132,6 +132,8 @@ def pcn_sweep(
     proposal="pcn",
     reg_scale=None,
     prior_chol=None,
+    samples=None,
+    sample_every=0,
 ):
     """In-place sweep on numpy arrays U [C, k] and phi [C] (dtype from U).
     proposal 'pcn': v = sqrt(1-beta^2) u + beta w; 'rw': v = u + beta w.
@@ -168,6 +170,12 @@ def pcn_sweep(
     s.n_steps = n_steps
     if sums is not None:
         s.sum_u, s.sum_u2 = _p(sums[0]), _p(sums[1])
+    if samples is not None:  # [C, n_samples, k]: in-launch samples every sample_every steps (0: the final state)
+        assert samples.flags.c_contiguous and samples.dtype == U.dtype and samples.shape[0] == U.shape[0]
+        s.sample_out = _p(samples)
+        s.sample_stride = samples.shape[1] * samples.shape[2]
+        s.sample_every = sample_every
+        s.sample_step_stride = samples.shape[2]
     rc = lib().orc_pcn_sweep(C.byref(m), C.byref(s), n_threads)
     assert rc == 0, rc
 

@@ -18,7 +18,7 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _sampler(op, y, gamma, var_step, chains_seed=5):
+def _sampler(op, y, gamma, var_step, chains_seed=5, **skw):
     from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
                              MCMCSampler, PhiloxRNG, VarSteppCNProposer, pCNAccepter)
 
@@ -26,41 +26,74 @@ def _sampler(op, y, gamma, var_step, chains_seed=5):
     pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(op.q), gamma**2 * np.eye(op.q)))
     prop = VarSteppCNProposer(lambda i: 0.1 + 0.4 / (1 + i), prior) if var_step else ConstSteppCNProposer(0.3, prior)
     acc = CountedAccepter(pCNAccepter(pot))
-    return MCMCSampler(prop, acc, PhiloxRNG(chains_seed)), acc
+    return MCMCSampler(prop, acc, PhiloxRNG(chains_seed), **skw), acc
 
 
-def _run(op, y, gamma, var_step, u0, keep, verbose, **kw):
-    s, acc = _sampler(op, y, gamma, var_step)
+def _run(op, y, gamma, var_step, u0, keep, verbose, skw, **kw):
+    s, acc = _sampler(op, y, gamma, var_step, **skw)
     s.verbose = verbose  # verbose keeps the per-sample launch loop (it prints every sample)
     with contextlib.redirect_stdout(io.StringIO()):
         out = s.run(u0, keep=keep, **kw)
     return out, np.asarray(acc.accepts), s.state.u
 
 
-@pytest.mark.parametrize("case", ["linear1", "linear4096", "l96", "l96_var"])
-@pytest.mark.parametrize("keep", ["samples", "moments"])
-def test_pcn_run_equals_per_sample_launches(dev, case, keep):
-    from ip_mcmc_amd import LinearOperator, Lorenz96Operator
+def _case(case, rng):
+    """(operator, data, noise std, chains, sampler options) of one kernel family."""
+    from ip_mcmc_amd import (BurgersOperator, LinearOperator, Lorenz63Operator, Lorenz96Operator,
+                             TwoScaleLorenz96Operator)
 
-    rng = np.random.default_rng(2)
     if case.startswith("linear"):
         op = LinearOperator(rng.normal(size=(3, 4)))
-        y, gamma = rng.normal(size=3), 0.5
-        n = 1 if case == "linear1" else 4096
-    else:
-        op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=50)
-        y, gamma = op(np.zeros(8)) + 0.1 * rng.normal(size=8), 0.2
-        n = 300
+        return op, rng.normal(size=3), 0.5, (1 if case == "linear1" else 4096), {}
+    if case == "l63":
+        op = Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=40)
+        return op, op(np.zeros(3)) + 0.2 * rng.normal(size=6), 0.5, 64, {}
+    if case == "burgers":
+        op = BurgersOperator(N=32, dt_mode="cfl", T=0.3)
+        return op, op(np.zeros(3)) + 0.05 * rng.normal(size=5), 0.1, 16, {}
+    if case == "ts":
+        op = TwoScaleLorenz96Operator(4, 2, dt=0.005, n_steps=40)
+        return op, op(np.zeros(3)) + 0.1 * rng.normal(size=op.q), 0.5, 40, {}
+    op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=50)
+    y = op(np.zeros(8)) + 0.1 * rng.normal(size=8)
+    skw = {}
+    if case in ("l96_seq", "l96_f32"):
+        skw["spec_width"] = 1  # the sequential kernels (packed pairs in f32)
+    if case == "l96_f32":
+        skw["dtype"] = np.float32
+    return op, y, 0.2, 300, skw
+
+
+@pytest.mark.parametrize("case", ["linear1", "linear4096", "l96", "l96_var", "l96_seq", "l96_f32", "l63", "burgers",
+                                  "ts"])
+@pytest.mark.parametrize("keep", ["samples", "moments"])
+def test_pcn_run_equals_per_sample_launches(dev, case, keep):
+    """In-launch samples (ipmc_sweep.sample_every, several samples per launch
+    through ipmc_pcn_run) equal one launch per sample, for every kernel
+    family: sequential, speculative, packed fp32."""
+    rng = np.random.default_rng(2)
+    op, y, gamma, n, skw = _case(case, rng)
     u0 = 0.1 * rng.normal(size=(n, op.k))
     kw = dict(n_samples=37, burn_in=25, sample_interval=6)
-    a = _run(op, y, gamma, case.endswith("var"), u0, keep, False, **kw)
-    b = _run(op, y, gamma, case.endswith("var"), u0, keep, True, **kw)
+    a = _run(op, y, gamma, case.endswith("var"), u0, keep, False, skw, **kw)
+    b = _run(op, y, gamma, case.endswith("var"), u0, keep, True, skw, **kw)
     if keep == "samples":
         assert a[0].shape == (n, 37, op.k) and np.array_equal(a[0], b[0])
     else:
         assert np.array_equal(a[0]["sum_u"], b[0]["sum_u"]) and np.array_equal(a[0]["sum_u2"], b[0]["sum_u2"])
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
     assert a[1].sum() > 0
+
+
+def test_interval_one_runs_across_sample_boundaries(dev):
+    """sample_interval=1 (the reference studies' recording): one chain still
+    runs multi-step launches (speculation across samples) with the same bits."""
+    rng = np.random.default_rng(6)
+    op, y, gamma, _, _ = _case("l96", rng)
+    u0 = 0.1 * rng.normal(size=op.k)
+    a = _run(op, y, gamma, False, u0, "samples", False, {}, n_samples=300, burn_in=0, sample_interval=1)
+    b = _run(op, y, gamma, False, u0, "samples", True, {}, n_samples=300, burn_in=0, sample_interval=1)
+    assert a[0].shape == (300, 8) and np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
 def test_pcn_run_streams_to_a_file(dev, tmp_path):

@@ -444,3 +444,32 @@ def test_lorenz63_oracle_is_textbook_rk4(orc, arith):
         g = orc.forward(op, u[None, :])[0]
         want = _l63_textbook(op.theta0 + u, op.x0, op.dt, op.n_steps)
         assert np.allclose(g, want, rtol=1e-11, atol=1e-11), (arith, u, g - want)
+
+
+@pytest.mark.parametrize("every", [1, 3, 7])
+def test_oracle_in_launch_samples_equal_per_sample_sweeps(orc, every):
+    """ipmc_sweep.sample_every (ABI 9): one sweep of n steps recording u after
+    every `every` steps equals n/every sweeps of `every` steps each recording
+    its final state (sampler.py:23-28), for the state, Φ and the counters."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=30)
+    rng = np.random.default_rng(4)
+    y, ginv = op.x0 + 0.3 * rng.normal(size=8), np.full(8, 4.0)
+    U0 = 0.2 * rng.normal(size=(5, 8))
+    phi0 = orc.potential(op, U0, y, ginv)
+    n = 21
+    U1, P1, A1 = U0.copy(), phi0.copy(), np.zeros(5, dtype=np.int64)
+    S1 = np.zeros((5, n // every, 8))
+    orc.pcn_sweep(op, U1, P1, y, ginv, np.ones(8), 0.4, 9, 100, n, accepts=A1, samples=S1, sample_every=every)
+    U2, P2, A2 = U0.copy(), phi0.copy(), np.zeros(5, dtype=np.int64)
+    S2 = np.zeros((5, n // every, 8))
+    for b in range(n // every):
+        one = np.zeros((5, 1, 8))
+        orc.pcn_sweep(op, U2, P2, y, ginv, np.ones(8), 0.4, 9, 100 + b * every, every, accepts=A2, samples=one)
+        S2[:, b] = one[:, 0]
+    rest = n - (n // every) * every
+    if rest:
+        orc.pcn_sweep(op, U2, P2, y, ginv, np.ones(8), 0.4, 9, 100 + n - rest, rest, accepts=A2)
+    assert np.array_equal(S1, S2) and np.array_equal(U1, U2) and np.array_equal(P1, P2) and np.array_equal(A1, A2)
+    assert A1.sum() > 0
