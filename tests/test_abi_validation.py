@@ -306,3 +306,22 @@ def test_pcn_run_validation(h):
     s.beta = 2.0  # the per-block checks of ipmc_pcn_sweep
     _status(h, h.ipmc_pcn_run(m, C.byref(s), 2, 3, 40, None), _abi.ERR_INVALID, "beta has to be in")
     assert h.ipmc_pcn_run(m, C.byref(_sweep()), 0, 5, 40, None) == _abi.OK  # no block: nothing to do
+
+
+def test_sample_every_validation(h):
+    """ipmc_sweep.sample_every (ABI 9): in-launch recording needs a sample
+    buffer whose rows and sample slots hold k values."""
+    m = C.byref(_model())
+    s = _sweep()
+    s.sample_every = -1
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_every must be in")
+    s.sample_every = 1 << 31
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_every must be in")
+    s.sample_every = 2
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_every needs sample_out")
+    s.sample_out, s.sample_stride, s.sample_step_stride = DUMMY, 400, 39
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_step_stride >= k")
+    s.sample_step_stride, s.sample_stride = 40, 39
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_stride >= k")
+    s.sample_stride, s.n_steps = 400, 0
+    assert h.ipmc_pcn_sweep(m, C.byref(s), None) == _abi.OK  # no step, no in-launch sample: nothing to copy

@@ -473,3 +473,22 @@ def test_oracle_in_launch_samples_equal_per_sample_sweeps(orc, every):
         orc.pcn_sweep(op, U2, P2, y, ginv, np.ones(8), 0.4, 9, 100 + n - rest, rest, accepts=A2)
     assert np.array_equal(S1, S2) and np.array_equal(U1, U2) and np.array_equal(P1, P2) and np.array_equal(A1, A2)
     assert A1.sum() > 0
+
+
+def test_oracle_in_launch_samples_edge_cases(orc):
+    """sample_every larger than the launch writes nothing; a launch that ends
+    between samples leaves the rest of the buffer untouched."""
+    from ip_mcmc_amd import LinearOperator
+
+    op = LinearOperator(np.array([[1.0, 2.0, 0.5]]))
+    U = np.zeros((3, 3))
+    P = orc.potential(op, U, np.array([1.0]), np.array([2.0]))
+    S = np.full((3, 4, 3), 7.0)
+    orc.pcn_sweep(op, U, P, [1.0], [2.0], np.ones(3), 0.5, 1, 0, 5, samples=S, sample_every=9)
+    assert np.all(S == 7.0)
+    U2 = np.zeros((3, 3))
+    P2 = orc.potential(op, U2, np.array([1.0]), np.array([2.0]))
+    orc.pcn_sweep(op, U2, P2, [1.0], [2.0], np.ones(3), 0.5, 1, 0, 7, samples=S, sample_every=3)
+    assert not np.all(S[:, :2] == 7.0) and np.all(S[:, 2:] == 7.0)  # samples after steps 3 and 6 only
+    with pytest.raises(AssertionError):  # the C oracle rejects a negative sample_every
+        orc.pcn_sweep(op, U2, P2, [1.0], [2.0], np.ones(3), 0.5, 1, 0, 7, samples=S, sample_every=-1)
