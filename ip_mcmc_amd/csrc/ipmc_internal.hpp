@@ -14,7 +14,7 @@ constexpr int kL96SpecBlockLanes = 256;
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 
-// Lorenz-96 dispatch (ipmc_l96_f32.hip / ipmc_l96_f64.hip).
+// Lorenz-96 dispatch (ipmc_l96_f{32,64}.hip; REFERENCE arith in ipmc_l96_f{32,64}_ref.hip).
 // Returns IPMC_ERR_UNSUPPORTED when (D, lpc) has no instantiation.
 // spec > 1: speculative sweep with `spec` slots per chain (one chain per lane group only).
 int l96_sweep_f32(const ipmc_model& m, const ipmc_sweep& s, int lpc, int cpl, int spec, hipStream_t st);

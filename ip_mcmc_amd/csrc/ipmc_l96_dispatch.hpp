@@ -88,11 +88,14 @@ int l96_sweep_pk_d(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_
   return l96_unsupported(m, lpc, "packed fp32 sweep");
 }
 
-inline int l96_sweep_pk(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
-  const bool fm = (m.arith == IPMC_ARITH_FMA);
+// The dispatchers below take the arithmetic mode as a template argument: each
+// (dtype, mode) pair is its own translation unit (ipmc_l96_f{32,64}{,_ref}.hip),
+// so the four build in parallel.
+template <bool FM>
+int l96_sweep_pk_f(const ipmc_model& m, const ipmc_sweep& s, int lpc, hipStream_t st) {
   switch (m.dim) {
 #define IPMC_DIM(D) \
-  case D: return fm ? l96_sweep_pk_d<D, true>(m, s, lpc, st) : l96_sweep_pk_d<D, false>(m, s, lpc, st);
+  case D: return l96_sweep_pk_d<D, FM>(m, s, lpc, st);
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }
@@ -113,28 +116,23 @@ int l96_eval_d(const ipmc_model& m, int64_t n, const void* u, const void* y, con
   return l96_unsupported(m, lpc, "evaluation");
 }
 
-template <typename T>
-int l96_sweep_t(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hipStream_t st) {
-  const bool fm = (m.arith == IPMC_ARITH_FMA);
+template <typename T, bool FM>
+int l96_sweep_tf(const ipmc_model& m, const ipmc_sweep& s, int lpc, int spec, hipStream_t st) {
   switch (m.dim) {
-#define IPMC_DIM(D)                                                                 \
-  case D:                                                                           \
-    return fm ? l96_sweep_d<T, D, true>(m, s, lpc, spec, st) : l96_sweep_d<T, D, false>(m, s, lpc, spec, st);
+#define IPMC_DIM(D) \
+  case D: return l96_sweep_d<T, D, FM>(m, s, lpc, spec, st);
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }
   return l96_unsupported(m, lpc, "dimension's");
 }
 
-template <typename T>
-int l96_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
-               int lpc, hipStream_t st) {
-  const bool fm = (m.arith == IPMC_ARITH_FMA);
+template <typename T, bool FM>
+int l96_eval_tf(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
+                int lpc, hipStream_t st) {
   switch (m.dim) {
-#define IPMC_DIM(D)                                                                  \
-  case D:                                                                            \
-    return fm ? l96_eval_d<T, D, true>(m, n, u, y, ginv, out, phi, lpc, st)          \
-              : l96_eval_d<T, D, false>(m, n, u, y, ginv, out, phi, lpc, st);
+#define IPMC_DIM(D) \
+  case D: return l96_eval_d<T, D, FM>(m, n, u, y, ginv, out, phi, lpc, st);
     IPMC_L96_DIMS(IPMC_DIM)
 #undef IPMC_DIM
   }

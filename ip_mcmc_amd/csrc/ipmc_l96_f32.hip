@@ -1,14 +1,22 @@
-// Lorenz-96 kernels, fp32 instantiations.
+// Lorenz-96 kernels, fp32 instantiations (one chain per lane group, and two
+// packed as f32x2), FMA arithmetic (REFERENCE: ipmc_l96_f32_ref.hip; one mode
+// per translation unit so they build in parallel).
 #include "ipmc_l96_dispatch.hpp"
 
 namespace ipmc {
 
+int l96_sweep_f32_ref(const ipmc_model& m, const ipmc_sweep& s, int lpc, int cpl, int spec, hipStream_t st);
+int l96_eval_f32_ref(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out,
+                     bool phi, int lpc, hipStream_t st);
+
 int l96_sweep_f32(const ipmc_model& m, const ipmc_sweep& s, int lpc, int cpl, int spec, hipStream_t st) {
-  return cpl == 2 ? l96_sweep_pk(m, s, lpc, st) : l96_sweep_t<float>(m, s, lpc, spec, st);
+  if (m.arith != IPMC_ARITH_FMA) return l96_sweep_f32_ref(m, s, lpc, cpl, spec, st);
+  return cpl == 2 ? l96_sweep_pk_f<true>(m, s, lpc, st) : l96_sweep_tf<float, true>(m, s, lpc, spec, st);
 }
 int l96_eval_f32(const ipmc_model& m, int64_t n, const void* u, const void* y, const void* ginv, void* out, bool phi,
                  int lpc, hipStream_t st) {
-  return l96_eval_t<float>(m, n, u, y, ginv, out, phi, lpc, st);
+  return m.arith == IPMC_ARITH_FMA ? l96_eval_tf<float, true>(m, n, u, y, ginv, out, phi, lpc, st)
+                                   : l96_eval_f32_ref(m, n, u, y, ginv, out, phi, lpc, st);
 }
 bool l96_has_f32(int D, int lpc, int cpl) {
   return cpl == 2 ? l96_has_t<double>(D, lpc) : l96_has_t<float>(D, lpc);
