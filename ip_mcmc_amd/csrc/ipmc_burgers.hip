@@ -65,6 +65,11 @@ __device__ __forceinline__ T rus_flux_fm(T a, T b, T c1, T c2, T cv = (T)0) {
   return madd<true>(s2, b - a, c1 * sq);
 }
 
+__device__ __forceinline__ double abs_of(double a) { return __builtin_fabs(a); }
+__device__ __forceinline__ float abs_of(float a) { return __builtin_fabsf(a); }
+__device__ __forceinline__ double max_of(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float max_of(float a, float b) { return __builtin_fmaxf(a, b); }
+
 template <int GS, typename T>
 __device__ __forceinline__ T group_max_abs(T m) {
 #pragma unroll
@@ -112,6 +117,40 @@ __device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const Ru
   }
 }
 
+// FMA arith in fp64: the flux in the scale F2 = F̃/c1 = 4F,
+//   F2(a, b) = fma(max(d_a, d_b), a − b, e_a + e_b),  e = w·w,  d = 2|w| [+ 4ν/dx],
+// with e and d formed once per cell (d as one fma with an abs source modifier,
+// so the viscous flux costs nothing), i.e. max, sub, add, fma per interface
+// (4 VALU ops instead of rus_flux_fm's 7); dudt = c1·(F2_{i+½} − F2_{i−½}) folds
+// c1 into the update's dt.  173 instead of 187 VALU instructions per SSPRK2
+// step and lane (8 cells); config 4 6-8 % faster (profiles/r2/burgers_f2_ab.jsonl).
+// fp32 keeps rus_flux_fm: the compiler packs that form into v_pk_* pairs, and
+// this one's shifted pairs cost ~45 repacking moves (measured 10-25 % slower).
+template <typename T, int CPL, bool VISC>
+__device__ __forceinline__ void rus_rate_f2(const T (&s)[CPL], T hl, T hr, T cv2, T (&r)[CPL]) {
+  T x[CPL + 2], e[CPL + 2], d[CPL + 2];
+  x[0] = hl;
+  x[CPL + 1] = hr;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) x[j + 1] = s[j];
+#pragma unroll
+  for (int i = 0; i < CPL + 2; ++i) {
+    e[i] = x[i] * x[i];
+    d[i] = VISC ? madd<true>(abs_of(x[i]), (T)2, cv2) : x[i] + x[i];
+  }
+  auto flux = [&](int i) {
+    const T sp = VISC ? max_of(d[i], d[i + 1]) : max_abs(d[i], d[i + 1]);
+    return madd<true>(sp, x[i] - x[i + 1], e[i] + e[i + 1]);
+  };
+  T fl = flux(0);
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const T fr = flux(j + 1);
+    r[j] = fr - fl;
+    fl = fr;
+  }
+}
+
 struct BurCtx {
   int sub, lane, nlive;
 };
@@ -152,6 +191,7 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   const T cfl_dx = (T)m.cfl * dx;
   const T rdx = (T)1 / mdx;
   const RusConst<T> kc{mdx, (T)0.25 * rdx, (T)-0.5 * rdx, (T)m.nu / (dx * dx)};
+  const T cv2 = ((T)4 * (T)m.nu) / dx;  // the viscous term in the F2 scale
   const T tend = (T)m.t_end;
   const T dtf = (T)m.dt;
   const bool cflmode = (m.dt_mode == IPMC_DT_CFL);
@@ -161,11 +201,19 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   // u* += dt L(u*); u = (u + u*)/2.  FMA arith folds the average into the
   // stages: u_half = fma(dt/2, L(u), u) next to u*, then
   // u = fma(dt/2, L(u*), u_half) (one VALU op per cell fewer; dt/2 is exact).
-  auto step = [&](T dt) {
+  constexpr bool F2 = FM && sizeof(T) == 8;
+  auto rate = [&](const T (&x)[CPL], T hl, T hr, T (&r)[CPL]) {
+    if constexpr (F2)
+      rus_rate_f2<T, CPL, VISC>(x, hl, hr, cv2, r);
+    else
+      rus_rate<T, CPL, FM, VISC>(x, hl, hr, kc, r);
+  };
+  auto step = [&](T dt0) {
     T hl, hr, r[CPL], ws[CPL];
+    const T dt = F2 ? dt0 * kc.c1 : dt0;  // F2: dudt = c1 ΔF2
     const T hdt = dt * (T)0.5;
     halos<T, CPL>(w, gl, gr, c, hl, hr);
-    rus_rate<T, CPL, FM, VISC>(w, hl, hr, kc, r);
+    rate(w, hl, hr, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       ws[j] = madd<FM>(dt, r[j], w[j]);
@@ -173,7 +221,7 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
     }
     const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
     halos<T, CPL>(ws, gls, grs, c, hl, hr);
-    rus_rate<T, CPL, FM, VISC>(ws, hl, hr, kc, r);
+    rate(ws, hl, hr, r);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       if constexpr (FM) {

@@ -27,21 +27,29 @@
 #define SFX(n) n##_f64
 #define FMA(a, b, c) fma((a), (b), (c))
 #define FMAX(a, b) fmax((a), (b))
+#define FABS(a) fabs(a)
+#define BUR_F2 1
 #include "orc_models.inc"
 #undef REAL
 #undef SFX
 #undef FMA
 #undef FMAX
+#undef FABS
+#undef BUR_F2
 
 #define REAL float
 #define SFX(n) n##_f32
 #define FMA(a, b, c) fmaf((a), (b), (c))
 #define FMAX(a, b) fmaxf((a), (b))
+#define FABS(a) fabsf(a)
+#define BUR_F2 0
 #include "orc_models.inc"
 #undef REAL
 #undef SFX
 #undef FMA
 #undef FMAX
+#undef FABS
+#undef BUR_F2
 
 static int check_model(const ipmc_model* m) {
   if (!m || m->k <= 0 || m->q <= 0) return IPMC_ERR_INVALID;
@@ -199,11 +207,20 @@ void orc_l96ts_rhs_f64(int32_t arith, int32_t K, int32_t J, const double* x, con
 }
 
 /* Rusanov pieces for the rusanov.py:112-170 known-answer tests. */
+/* FMA arith: the fp64 kernels' F2 flux and rate, in the reference's units
+ * (F = F2/4, dudt = c1 (F2_{i+1/2} - F2_{i-1/2})). */
 double orc_rusanov_flux_f64(int32_t arith, double a, double b) {
-  return arith == IPMC_ARITH_FMA ? rus_flux_fm_f64(a, b, 0.25, -0.5, 0, 0.0) : rus_flux_f64(a, b);
+  if (arith != IPMC_ARITH_FMA) return rus_flux_f64(a, b);
+  return 0.25 * fma(fmax(fabs(a + a), fabs(b + b)), a - b, a * a + b * b); /* rus_rate_f2 */
 }
 void orc_rusanov_rate_f64(int32_t arith, int32_t N, const double* w, double dx, double* r) {
-  rus_rate_f64(arith == IPMC_ARITH_FMA, N, w, -dx, 0.0, 0, r);
+  if (arith != IPMC_ARITH_FMA) {
+    rus_rate_f64(0, N, w, -dx, 0.0, 0, r);
+    return;
+  }
+  const double c1 = 0.25 * (1.0 / -dx);
+  rus_rate_f2_f64(N, w, 0, 0.0, r);
+  for (int i = 1; i <= N; ++i) r[i] = c1 * r[i];
 }
 
 

@@ -242,6 +242,18 @@ def test_rusanov_kats(orc, golden):
     assert np.array_equal(r[1:-1], golden["rus_rate_out"])
 
 
+def test_rusanov_kats_fma_arith(orc, golden):
+    """The fp64 kernels' FMA-arith flux (the F2 = 4F scale, rus_rate_f2) on the
+    same known answers: exact on these small integers, the rates within a few
+    ulps of the reference's."""
+    for (a, b), want in zip(golden["rus_kat_flux_in"], golden["rus_kat_flux_out"]):
+        assert orc.rusanov_flux(a, b, "fma") == want
+    r = orc.rusanov_rate(golden["rus_kat_rate_in"], golden["rus_kat_rate_dx"][0], "fma")
+    np.testing.assert_allclose(r[1:-1], golden["rus_kat_rate_out"], rtol=1e-14)
+    r = orc.rusanov_rate(golden["rus_rate_w"], golden["rus_rate_dx"][0], "fma")
+    np.testing.assert_allclose(r[1:-1], golden["rus_rate_out"], rtol=1e-12, atol=1e-12)
+
+
 @pytest.mark.parametrize("N", [32, 128, 256])
 def test_burgers_forward_reference_bit_exact(orc, golden, N):
     """FVMObservationOperator = Measurer(RusanovFVM.integrate(IC)) of the reference vs the oracle, fp64, CFL dt."""
