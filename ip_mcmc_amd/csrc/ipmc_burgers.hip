@@ -48,23 +48,6 @@ __device__ __forceinline__ float max_abs(float a, float b) {
   return r;
 }
 
-// FMA arith: the flux pre-scaled by 1/(−dx), F̃ = fma(c2·s, b−a, c1·(a²+b²))
-// with c1 = ¼/(−dx), c2 = −½/(−dx), so dudt = F̃_{i+½} − F̃_{i−½} needs no
-// division (7 VALU ops per interface).  max is fmax: equal to the reference's
-// max for every non-NaN pair.  VISC adds the viscous flux −ν(b−a)/dx in the
-// same pre-scaled form, ν/dx²·(b−a), by folding ν/dx² into the wave-speed
-// coefficient: fma(fma(c2, s, ν/dx²), b−a, c1·(a²+b²)) -- the same 7 ops, so
-// the difference of neighbouring fluxes is the central-difference Laplacian
-// ν(u_{i+1} − 2u_i + u_{i−1})/dx² at no extra cost (the central-difference
-// form took 4 more VALU ops per cell and stage: cfg 4 0.44 -> 0.55 ms).
-template <typename T, bool VISC = false>
-__device__ __forceinline__ T rus_flux_fm(T a, T b, T c1, T c2, T cv = (T)0) {
-  const T sp = max_abs(a, b);
-  const T sq = madd<true>(b, b, a * a);
-  const T s2 = VISC ? madd<true>(c2, sp, cv) : c2 * sp;
-  return madd<true>(s2, b - a, c1 * sq);
-}
-
 __device__ __forceinline__ double abs_of(double a) { return __builtin_fabs(a); }
 __device__ __forceinline__ float abs_of(float a) { return __builtin_fabsf(a); }
 __device__ __forceinline__ double max_of(double a, double b) { return __builtin_fmax(a, b); }
@@ -92,23 +75,23 @@ __device__ __forceinline__ T lane_max_abs(const T (&w)[CPL], bool live) {
   return m;
 }
 
-// dudt for the lane's cells from state s (+ halos hl / hr).
-// k.mdx = −dx (REFERENCE divides by it); k.c1, k.c2: the FMA flux scales.
+// REFERENCE arith: dudt = (F_{i+½} − F_{i−½})/(−dx) for the lane's cells from
+// state s (+ halos hl / hr); VISC adds ν(u_{i+1} − 2u_i + u_{i−1})/dx².
 template <typename T>
 struct RusConst {
-  T mdx, c1, c2, nudx2;
+  T mdx, c1, nudx2;  // −dx, the F2 scale ¼/(−dx), ν/dx²
 };
 
-template <typename T, int CPL, bool FM, bool VISC>
+template <typename T, int CPL, bool VISC>
 __device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const RusConst<T>& k, T (&r)[CPL]) {
-  T fl = FM ? rus_flux_fm<T, VISC>(hl, s[0], k.c1, k.c2, k.nudx2) : rus_flux_ref<T>(hl, s[0]);
+  T fl = rus_flux_ref<T>(hl, s[0]);
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const T right = (j + 1 < CPL) ? s[j + 1] : hr;
     const T left = (j > 0) ? s[j - 1] : hl;
-    const T fr = FM ? rus_flux_fm<T, VISC>(s[j], right, k.c1, k.c2, k.nudx2) : rus_flux_ref<T>(s[j], right);
-    T v = FM ? fr - fl : (fr - fl) / k.mdx;
-    if (VISC && !FM) {  // REFERENCE arith: the central-difference form
+    const T fr = rus_flux_ref<T>(s[j], right);
+    T v = (fr - fl) / k.mdx;
+    if (VISC) {  // the central-difference form
       const T lap = (right - (s[j] + s[j])) + left;
       v = v + k.nudx2 * lap;
     }
@@ -117,15 +100,16 @@ __device__ __forceinline__ void rus_rate(const T (&s)[CPL], T hl, T hr, const Ru
   }
 }
 
-// FMA arith in fp64: the flux in the scale F2 = F̃/c1 = 4F,
+// FMA arith: the flux in the scale F2 = 4F,
 //   F2(a, b) = fma(max(d_a, d_b), a − b, e_a + e_b),  e = w·w,  d = 2|w| [+ 4ν/dx],
 // with e and d formed once per cell (d as one fma with an abs source modifier,
-// so the viscous flux costs nothing), i.e. max, sub, add, fma per interface
-// (4 VALU ops instead of rus_flux_fm's 7); dudt = c1·(F2_{i+½} − F2_{i−½}) folds
-// c1 into the update's dt.  173 instead of 187 VALU instructions per SSPRK2
-// step and lane (8 cells); config 4 6-8 % faster (profiles/r2/burgers_f2_ab.jsonl).
-// fp32 keeps rus_flux_fm: the compiler packs that form into v_pk_* pairs, and
-// this one's shifted pairs cost ~45 repacking moves (measured 10-25 % slower).
+// so the viscous flux costs nothing), i.e. max, sub, add, fma per interface,
+// and dudt = c1·(F2_{i+½} − F2_{i−½}), c1 = ¼/(−dx), folded into the update's
+// dt.  In fp64 an SSPRK2 step takes 173 VALU instructions per lane of 8 cells
+// (187 with the earlier pre-scaled flux fma(c2·s, b−a, c1·(a²+b²)), 7 ops per
+// interface; profiles/r2/burgers_f2_ab.jsonl).  fp32 runs the same arithmetic
+// on cell pairs (rus_rate_pk).  The flux differences of the viscous term are
+// the central-difference Laplacian; REFERENCE arith keeps that form.
 template <typename T, int CPL, bool VISC>
 __device__ __forceinline__ void rus_rate_f2(const T (&s)[CPL], T hl, T hr, T cv2, T (&r)[CPL]) {
   T x[CPL + 2], e[CPL + 2], d[CPL + 2];
@@ -170,6 +154,40 @@ __device__ __forceinline__ void halos(const T (&s)[CPL], T gl, T gr, const BurCt
   if (c.sub == c.nlive - 1) hr = gr;
 }
 
+// fp32 FMA arith: rus_rate_f2 on cell pairs P[p] = (w[p], w[p+H]), H = CPL/2,
+// so every flux, rate and update is a v_pk_*_f32 on two cells (the max is two
+// v_max_f32 with abs modifiers: there is no packed max).  Pair p's neighbours
+// are pairs p-1 and p+1 except at the ends: Q = [(hl, w[H-1]), P[0..H-1],
+// (w[H], hr)], so the interface w[H-1]|w[H] is evaluated twice, bit-identically.
+// The viscous wave speed max(2|a|, 2|b|) + 4ν/dx equals rus_rate_f2's
+// max(fma(|a|, 2, 4ν/dx), fma(|b|, 2, 4ν/dx)) exactly (2|w| is exact and
+// rounding is monotone).
+template <int H, bool VISC>
+__device__ __forceinline__ void rus_rate_pk(const f32x2 (&X)[H], float hl, float hr, f32x2 cv2, f32x2 (&r)[H]) {
+  f32x2 q[H + 2], e[H + 2], d[H + 2];
+  q[0] = f32x2{hl, X[H - 1].x};
+#pragma unroll
+  for (int p = 0; p < H; ++p) q[p + 1] = X[p];
+  q[H + 1] = f32x2{X[0].y, hr};
+#pragma unroll
+  for (int i = 0; i < H + 2; ++i) {
+    e[i] = q[i] * q[i];
+    d[i] = q[i] + q[i];
+  }
+  auto flux = [&](int i) {
+    f32x2 sp = f32x2{max_abs(d[i].x, d[i + 1].x), max_abs(d[i].y, d[i + 1].y)};
+    if (VISC) sp = sp + cv2;
+    return madd<true>(sp, q[i] - q[i + 1], e[i] + e[i + 1]);
+  };
+  f32x2 fl = flux(0);
+#pragma unroll
+  for (int p = 0; p < H; ++p) {
+    const f32x2 fr = flux(p + 1);
+    r[p] = fr - fl;
+    fl = fr;
+  }
+}
+
 // Integrate the Riemann IC (left, right, jump) to the end; returns validity.
 // w holds the final interior cells of this lane.  VISC is a compile-time
 // switch: a runtime flag made the compiler evaluate the diffusion term for
@@ -190,7 +208,7 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   const T dx = (T)m.dx, mdx = -dx;
   const T cfl_dx = (T)m.cfl * dx;
   const T rdx = (T)1 / mdx;
-  const RusConst<T> kc{mdx, (T)0.25 * rdx, (T)-0.5 * rdx, (T)m.nu / (dx * dx)};
+  const RusConst<T> kc{mdx, (T)0.25 * rdx, (T)m.nu / (dx * dx)};
   const T cv2 = ((T)4 * (T)m.nu) / dx;  // the viscous term in the F2 scale
   const T tend = (T)m.t_end;
   const T dtf = (T)m.dt;
@@ -200,39 +218,82 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
   // One SSPRK2 step of size dt, rusanov.py:62-74.  REFERENCE: u* = u + dt L(u);
   // u* += dt L(u*); u = (u + u*)/2.  FMA arith folds the average into the
   // stages: u_half = fma(dt/2, L(u), u) next to u*, then
-  // u = fma(dt/2, L(u*), u_half) (one VALU op per cell fewer; dt/2 is exact).
-  constexpr bool F2 = FM && sizeof(T) == 8;
-  auto rate = [&](const T (&x)[CPL], T hl, T hr, T (&r)[CPL]) {
-    if constexpr (F2)
-      rus_rate_f2<T, CPL, VISC>(x, hl, hr, cv2, r);
-    else
-      rus_rate<T, CPL, FM, VISC>(x, hl, hr, kc, r);
-  };
+  // u = fma(dt/2, L(u*), u_half) (one VALU op per cell fewer; dt/2 is exact),
+  // with dt scaled by c1 for the F2 flux (dudt = c1 ΔF2).
+  constexpr bool PK = FM && sizeof(T) == 4;
+  constexpr int H = CPL / 2;
+  f32x2 P[H];  // PK: the state as cell pairs (w[p], w[p+H])
+  if constexpr (PK) {
+#pragma unroll
+    for (int p = 0; p < H; ++p) P[p] = f32x2{(float)w[p], (float)w[p + H]};
+  }
   auto step = [&](T dt0) {
-    T hl, hr, r[CPL], ws[CPL];
-    const T dt = F2 ? dt0 * kc.c1 : dt0;  // F2: dudt = c1 ΔF2
+    const T dt = FM ? dt0 * kc.c1 : dt0;
     const T hdt = dt * (T)0.5;
-    halos<T, CPL>(w, gl, gr, c, hl, hr);
-    rate(w, hl, hr, r);
+    if constexpr (PK) {
+      const f32x2 dtv{(float)dt, (float)dt}, hdtv{(float)hdt, (float)hdt}, cvv{(float)cv2, (float)cv2};
+      f32x2 r[H], S[H];
+      float hl = dpp<kDppWaveShr1>(P[H - 1].y), hr = dpp<kDppWaveShl1>(P[0].x);
+      if (c.sub == 0) hl = (float)gl;
+      if (c.sub == c.nlive - 1) hr = (float)gr;
+      rus_rate_pk<H, VISC>(P, hl, hr, cvv, r);
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      ws[j] = madd<FM>(dt, r[j], w[j]);
-      if constexpr (FM) w[j] = madd<true>(hdt, r[j], w[j]);
-    }
-    const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
-    halos<T, CPL>(ws, gls, grs, c, hl, hr);
-    rate(ws, hl, hr, r);
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      if constexpr (FM) {
-        w[j] = madd<true>(hdt, r[j], w[j]);
-      } else {
-        ws[j] = ws[j] + dt * r[j];
-        w[j] = (w[j] + ws[j]) / (T)2;
+      for (int p = 0; p < H; ++p) {
+        S[p] = madd<true>(dtv, r[p], P[p]);
+        P[p] = madd<true>(hdtv, r[p], P[p]);
       }
+      hl = dpp<kDppWaveShr1>(S[H - 1].y);
+      hr = dpp<kDppWaveShl1>(S[0].x);
+      if (c.sub == 0) hl = S[0].x;  // BC on u*
+      if (c.sub == c.nlive - 1) hr = S[H - 1].y;
+      rus_rate_pk<H, VISC>(S, hl, hr, cvv, r);
+#pragma unroll
+      for (int p = 0; p < H; ++p) P[p] = madd<true>(hdtv, r[p], P[p]);
+      gl = P[0].x;
+      gr = P[H - 1].y;
+    } else {
+      T hl, hr, r[CPL], ws[CPL];
+      halos<T, CPL>(w, gl, gr, c, hl, hr);
+      if constexpr (FM)
+        rus_rate_f2<T, CPL, VISC>(w, hl, hr, cv2, r);
+      else
+        rus_rate<T, CPL, VISC>(w, hl, hr, kc, r);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        ws[j] = madd<FM>(dt, r[j], w[j]);
+        if constexpr (FM) w[j] = madd<true>(hdt, r[j], w[j]);
+      }
+      const T gls = ws[0], grs = ws[CPL - 1];  // BC on u*, used by the first / last live lane only
+      halos<T, CPL>(ws, gls, grs, c, hl, hr);
+      if constexpr (FM)
+        rus_rate_f2<T, CPL, VISC>(ws, hl, hr, cv2, r);
+      else
+        rus_rate<T, CPL, VISC>(ws, hl, hr, kc, r);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        if constexpr (FM) {
+          w[j] = madd<true>(hdt, r[j], w[j]);
+        } else {
+          ws[j] = ws[j] + dt * r[j];
+          w[j] = (w[j] + ws[j]) / (T)2;
+        }
+      }
+      gl = w[0];
+      gr = w[CPL - 1];
     }
-    gl = w[0];
-    gr = w[CPL - 1];
+  };
+  // max|w| over the lane's cells (order-free: maxNum of absolute values)
+  auto lane_max = [&]() -> T {
+    if constexpr (PK) {
+      float mx = 0.0f;
+      if (live) {
+#pragma unroll
+        for (int p = 0; p < H; ++p) mx = max_abs(max_abs(mx, P[p].x), P[p].y);
+      }
+      return (T)mx;
+    } else {
+      return lane_max_abs<CPL>(w, live);
+    }
   };
   if (cflmode) {
     // dt = cfl dx / max|w| over the group each step, while t < t_end (the
@@ -240,7 +301,7 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
     T t = (T)0;
     int iters = 0;
     for (;;) {
-      const T mx = group_max_abs<GS>(lane_max_abs<CPL>(w, live));
+      const T mx = group_max_abs<GS>(lane_max());
       if (!(t < tend)) break;
       if (iters >= m.max_iter) {
         valid = false;
@@ -255,9 +316,16 @@ __device__ bool burgers_integrate(const ipmc_model& m, T left, T right, T jump, 
     // fixed dt: a uniform trip count, and a per-lane CFL guard reduced once
     const int n = m.n_steps;
     for (int it = 0; it < n; ++it) {
-      const T mx = lane_max_abs<CPL>(w, live);
+      const T mx = lane_max();
       if (!(mx * dtf <= cfl_dx)) lane_ok = false;
       step(dtf);
+    }
+  }
+  if constexpr (PK) {
+#pragma unroll
+    for (int p = 0; p < H; ++p) {
+      w[p] = P[p].x;
+      w[p + H] = P[p].y;
     }
   }
   if (!cflmode) {

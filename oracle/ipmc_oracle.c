@@ -28,28 +28,24 @@
 #define FMA(a, b, c) fma((a), (b), (c))
 #define FMAX(a, b) fmax((a), (b))
 #define FABS(a) fabs(a)
-#define BUR_F2 1
 #include "orc_models.inc"
 #undef REAL
 #undef SFX
 #undef FMA
 #undef FMAX
 #undef FABS
-#undef BUR_F2
 
 #define REAL float
 #define SFX(n) n##_f32
 #define FMA(a, b, c) fmaf((a), (b), (c))
 #define FMAX(a, b) fmaxf((a), (b))
 #define FABS(a) fabsf(a)
-#define BUR_F2 0
 #include "orc_models.inc"
 #undef REAL
 #undef SFX
 #undef FMA
 #undef FMAX
 #undef FABS
-#undef BUR_F2
 
 static int check_model(const ipmc_model* m) {
   if (!m || m->k <= 0 || m->q <= 0) return IPMC_ERR_INVALID;
@@ -207,7 +203,7 @@ void orc_l96ts_rhs_f64(int32_t arith, int32_t K, int32_t J, const double* x, con
 }
 
 /* Rusanov pieces for the rusanov.py:112-170 known-answer tests. */
-/* FMA arith: the fp64 kernels' F2 flux and rate, in the reference's units
+/* FMA arith: the kernels' F2 flux and rate, in the reference's units
  * (F = F2/4, dudt = c1 (F2_{i+1/2} - F2_{i-1/2})). */
 double orc_rusanov_flux_f64(int32_t arith, double a, double b) {
   if (arith != IPMC_ARITH_FMA) return rus_flux_f64(a, b);
@@ -215,7 +211,7 @@ double orc_rusanov_flux_f64(int32_t arith, double a, double b) {
 }
 void orc_rusanov_rate_f64(int32_t arith, int32_t N, const double* w, double dx, double* r) {
   if (arith != IPMC_ARITH_FMA) {
-    rus_rate_f64(0, N, w, -dx, 0.0, 0, r);
+    rus_rate_f64(N, w, -dx, 0.0, 0, r);
     return;
   }
   const double c1 = 0.25 * (1.0 / -dx);

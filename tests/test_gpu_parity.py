@@ -410,6 +410,9 @@ def test_burgers_forward_potential_bit_exact(dev, orc, dtype):
         U = 0.25 * rng.normal(size=(96, 3))
         U[0] = 0.0
         U[1] = [3.0, 0.0, 0.0]  # fast left state: violates the fixed-dt CFL guard
+        # the jump inside the first / last cell: an IC ghost unlike its neighbour cell
+        U[2] = [0.0, 0.0, -1.0 - op.theta0[2]]
+        U[3] = [0.0, 0.0, 1.0 - op.theta0[2]]
         g = op.forward_device(_t(U, dtype, dev)).cpu().numpy()
         go = orc.forward(op, U, _np(dtype))
         assert np.array_equal(g, go, equal_nan=True), (op.N, op.dt_mode, op.arith, np.nanmax(np.abs(g - go)))
@@ -680,18 +683,22 @@ def test_f32_and_f64_posterior_means_agree(dev):
     assert np.all(z < 4), z
 
 
-def test_burgers_every_layout_bit_exact(dev, orc):
-    """Both cells-per-lane layouts (8 and 4) of the Burgers kernel give the oracle's bits."""
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_burgers_every_layout_bit_exact(dev, orc, dtype):
+    """Both cells-per-lane layouts (8 and 4; in fp32 FMA arith 4 and 2 cell
+    pairs per lane) of the Burgers kernel give the oracle's bits, inviscid and
+    viscous."""
     from ip_mcmc_amd import BurgersOperator
 
     for N, lanes_list in ((128, (16, 32)), (256, (32, 64))):
         for arith in ("fma", "reference"):
-            op = BurgersOperator(N=N, dt_mode="cfl", arith=arith)
-            U0, phi0, y, ginv, sq = _problem(op, 40, torch.float64, orc, seed=N)
-            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, torch.float64)
-            for lanes in lanes_list:
-                d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, torch.float64, dev, lanes=lanes)
-                _assert_same(d, o, (N, arith, lanes))
+            for nu in (0.0, 1e-3):
+                op = BurgersOperator(N=N, dt_mode="cfl", arith=arith, nu=nu)
+                U0, phi0, y, ginv, sq = _problem(op, 40, dtype, orc, seed=N)
+                o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, dtype)
+                for lanes in lanes_list:
+                    d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.15, 3, 0, 3, dtype, dev, lanes=lanes)
+                    _assert_same(d, o, (N, arith, nu, lanes))
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
