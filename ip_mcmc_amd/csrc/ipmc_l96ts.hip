@@ -17,6 +17,10 @@ namespace ipmc {
 
 constexpr int kTsBlock = 256;
 
+#ifndef IPMC_TS_PK
+#define IPMC_TS_PK 1
+#endif
+
 // Occupancy target (waves per SIMD) for the sweep kernel: 4 RK4 arrays of
 // 1 + J values per lane plus the chain state.
 template <typename T, int J, int SPL>
@@ -207,6 +211,173 @@ __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + 
   }
 }
 
+// fp32 with J even: each fast block held as H = J/2 pairs of f32x2,
+// Y[p] = (Y_{k,p}, Y_{k,p+H}), so the fast rates and RK4 updates are
+// v_pk_*_f32 on two fast variables.  The block's cyclic neighbours of pair p
+// are pairs p±1, p+2 with the halves swapped each time the index wraps past H
+// (ts_pair); every per-element operation is the scalar kernel's, so the bits
+// are the same (the block sum / mean still adds the scalars in numpy's order).
+template <int H>
+__device__ __forceinline__ f32x2 ts_pair(const f32x2 (&y)[H], const f32x2& old0, const f32x2& old1, int i) {
+  // pair i of the cyclic sequence, i in [-1, H + 1]; indices >= H read the
+  // saved old pairs 0 / 1 (the in-place stage has overwritten them)
+  const int w = i < 0 ? -1 : i / H;
+  const int j = i - w * H;
+  const f32x2 v = (w >= 1) ? (j == 0 ? old0 : old1) : y[j];
+  return (w & 1) ? __builtin_shufflevector(v, v, 1, 0) : v;
+}
+
+template <int J>
+__device__ __forceinline__ float ts_pk_sum(const f32x2 (&y)[J / 2], bool mean) {
+  constexpr int H = J / 2;
+  float a[J];
+#pragma unroll
+  for (int p = 0; p < H; ++p) {
+    a[p] = y[p].x;
+    a[p + H] = y[p].y;
+  }
+  const float sm = np_pairwise<float, J>(a, 0);
+  return mean ? sm / (float)J : sm;
+}
+
+template <int J, bool FM, int SPL, int STAGE>
+__device__ __forceinline__ void ts_stage_pk(float (&xin)[SPL], f32x2 (&yin)[SPL][J / 2], float (&xout)[SPL],
+                                            f32x2 (&yout)[SPL][J / 2], float (&xb)[SPL], f32x2 (&yb)[SPL][J / 2],
+                                            float (&xa)[SPL], f32x2 (&ya)[SPL][J / 2], float cst,
+                                            const TsCoef<float>& kc, const TsCoef<f32x2>& kv, const TsCtx& c) {
+  constexpr int H = J / 2;
+  auto upd = [&](auto& acc, auto& out, const auto& base, auto k, auto cs) {
+    using V = decltype(k);
+    if constexpr (STAGE == 1) acc = k;
+    else if constexpr (STAGE == 4) acc = acc + k;
+    else acc = madd<FM>(Splat<V>::of(2.0f), k, acc);
+    if constexpr (STAGE == 4) out = madd<FM>(cs, acc, base);
+    else out = madd<FM>(cs, k, base);
+  };
+  const f32x2 csv{cst, cst};
+  const int L = c.K / SPL;
+  float Xo[SPL], ybk[SPL], kX[SPL];
+#pragma unroll
+  for (int a = 0; a < SPL; ++a) {
+    Xo[a] = xin[a];
+    ybk[a] = ts_pk_sum<J>(yin[a], !FM);
+  }
+  if constexpr (SPL == 1) {
+    const float xm1 = __shfl(Xo[0], c.base + (c.sub + L - 1) % L, 64);
+    const float xm2 = __shfl(Xo[0], c.base + (c.sub + L - 2) % L, 64);
+    const float xp1 = __shfl(Xo[0], c.base + (c.sub + 1) % L, 64);
+    kX[0] = ts_slow<float, FM>(Xo[0], xm1, xm2, xp1, kc, ybk[0]);
+  } else {
+    const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
+    const float p1 = __shfl(Xo[SPL - 1], prev, 64);
+    const float p2 = __shfl(Xo[SPL - 2], prev, 64);
+    const float n0 = __shfl(Xo[0], next, 64);
+#pragma unroll
+    for (int a = 0; a < SPL; ++a) {
+      const float xm1 = a >= 1 ? Xo[a - 1] : p1;
+      const float xm2 = a >= 2 ? Xo[a - 2] : (a == 1 ? p1 : p2);
+      const float xp1 = a + 1 < SPL ? Xo[a + 1] : n0;
+      kX[a] = ts_slow<float, FM>(Xo[a], xm1, xm2, xp1, kc, ybk[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < SPL; ++a) {
+    upd(xa[a], xout[a], xb[a], kX[a], cst);
+    const f32x2 Xv{Xo[a], Xo[a]};
+    const float q = FM ? kc.chJ * Xo[a] : 0.0f;
+    const f32x2 qX{q, q};
+    const f32x2 old0 = yin[a][0], old1 = yin[a][1 % H];
+    f32x2 prevp = ts_pair<H>(yin[a], old0, old1, -1);  // old pair -1 (= pair H-1, swapped)
+#pragma unroll
+    for (int p = 0; p < H; ++p) {
+      const f32x2 y = yin[a][p];  // pairs >= p are not yet overwritten
+      const f32x2 yp1 = ts_pair<H>(yin[a], old0, old1, p + 1);
+      const f32x2 yp2 = ts_pair<H>(yin[a], old0, old1, p + 2);
+      const f32x2 k = ts_fast<f32x2, FM>(y, yp1, yp2, prevp, Xv, qX, kv);
+      prevp = y;
+      upd(ya[a][p], yout[a][p], yb[a][p], k, csv);
+    }
+  }
+}
+
+// ts_phi for fp32 with J even: the fast blocks as pairs (ts_stage_pk).
+template <int J, bool FM, int SPL>
+__device__ float ts_phi_pk(const ipmc_model& m, const float (&v)[3], const TsCtx& c, int kq, const float* __restrict__ y,
+                           const float* __restrict__ ginv, float* g_out) {
+  constexpr int H = J / 2;
+  const int K = c.K;
+  const int k0 = kq * SPL;
+  const float* th0 = (const float*)m.theta0;
+  const float F = th0[0] + v[0], h = th0[1] + v[1], bb = th0[2] + v[2];
+  const TsCoef<float> kc = ts_coef<float>(F, h, bb, (float)m.coupling_c, J);
+  TsCoef<f32x2> kv;
+  kv.F = f32x2{kc.F, kc.F};
+  kv.hc = f32x2{kc.hc, kc.hc};
+  kv.hJ = f32x2{kc.hJ, kc.hJ};
+  kv.bb = f32x2{kc.bb, kc.bb};
+  kv.cc = f32x2{kc.cc, kc.cc};
+  kv.hcJ = f32x2{kc.hcJ, kc.hcJ};
+  kv.chJ = f32x2{kc.chJ, kc.chJ};
+  kv.cb = f32x2{kc.cb, kc.cb};
+  const float rJ = 1.0f / (float)J;
+  const float hh = (float)m.dt, h2 = hh * 0.5f, h6 = hh / 6.0f;
+  const float* x0 = (const float*)m.x0;
+  float X[SPL], ob[SPL][5];
+  f32x2 Y[SPL][H];
+#pragma unroll
+  for (int i = 0; i < SPL; ++i) {
+    X[i] = x0[k0 + i];
+    const float* yb0 = x0 + K + (k0 + i) * J;
+#pragma unroll
+    for (int p = 0; p < H; ++p) Y[i][p] = f32x2{yb0[p], yb0[p + H]};
+#pragma unroll
+    for (int b = 0; b < 5; ++b) ob[i][b] = 0.0f;
+  }
+  const bool refmom = (m.moment_mode == 0);
+  for (int n = 0; n < m.n_steps; ++n) {
+    float xa[SPL], xs[SPL];
+    f32x2 ya[SPL][H], ys[SPL][H];
+    ts_stage_pk<J, FM, SPL, 1>(X, Y, xs, ys, X, Y, xa, ya, h2, kc, kv, c);
+    ts_stage_pk<J, FM, SPL, 2>(xs, ys, xs, ys, X, Y, xa, ya, h2, kc, kv, c);
+    ts_stage_pk<J, FM, SPL, 3>(xs, ys, xs, ys, X, Y, xa, ya, hh, kc, kv, c);
+    ts_stage_pk<J, FM, SPL, 4>(xs, ys, X, Y, X, Y, xa, ya, h6, kc, kv, c);
+#pragma unroll
+    for (int a = 0; a < SPL; ++a) {
+      const float Xa = X[a];
+      const float yb = refmom ? Y[a][0].x : (FM ? ts_pk_sum<J>(Y[a], false) * rJ : ts_pk_sum<J>(Y[a], true));
+      ob[a][0] = ob[a][0] + Xa;
+      ob[a][1] = ob[a][1] + yb;
+      ob[a][2] = madd<FM>(Xa, Xa, ob[a][2]);
+      ob[a][3] = madd<FM>(Xa, yb, ob[a][3]);
+      ob[a][4] = madd<FM>(yb, yb, ob[a][4]);
+    }
+  }
+  const float nn = (float)m.n_steps;
+  float r[SPL][5];
+#pragma unroll
+  for (int a = 0; a < SPL; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const int k = k0 + a;
+      const float g = ob[a][b] / nn;
+      if (g_out) g_out[b * K + k] = g;
+      r[a][b] = y ? (y[b * K + k] - g) * ginv[b * K + k] : 0.0f;
+    }
+  float s = 0.0f;
+  if (y) {
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      for (int kk = 0; kk < K; ++kk) {  // observation order: slow variable kk of moment b
+        float mine = r[0][b];
+        if constexpr (SPL == 2) mine = (kk & 1) ? r[1][b] : r[0][b];
+        const float val = __shfl(mine, c.base + kk / SPL, 64);
+        s = madd<FM>(val, val, s);
+      }
+    }
+  }
+  return 0.5f * s;
+}
+
 // Φ(theta0 + v) for the group; g_out (per chain, [5K]) receives G if set.
 // kq: k behind an opaque register copy made once per pCN step, so the
 // per-lane constants (x0 block, y, 1/gamma) are re-read each step instead of
@@ -214,6 +385,8 @@ __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + 
 template <typename T, int J, bool FM, int SPL>
 __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq, const T* __restrict__ y,
                     const T* __restrict__ ginv, T* g_out) {
+  if constexpr (sizeof(T) == 4 && J % 2 == 0 && IPMC_TS_PK)
+    return ts_phi_pk<J, FM, SPL>(m, v, c, kq, y, ginv, g_out);
   const int K = c.K;
   const int k0 = kq * SPL;  // this lane's first slow variable
   const T* th0 = (const T*)m.theta0;
