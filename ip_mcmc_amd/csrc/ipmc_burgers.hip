@@ -53,13 +53,37 @@ __device__ __forceinline__ float abs_of(float a) { return __builtin_fabsf(a); }
 __device__ __forceinline__ double max_of(double a, double b) { return __builtin_fmax(a, b); }
 __device__ __forceinline__ float max_of(float a, float b) { return __builtin_fmaxf(a, b); }
 
+// ds_swizzle in bit mode (and 0x1F, xor 0x10): lane i reads lane i ^ 16 of
+// its 32-lane half; no address operand, no LDS storage.
+__device__ __forceinline__ float swz_xor16(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+}
+__device__ __forceinline__ double swz_xor16(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)(b & 0xffffffff), 0x401F);
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// max over the GS-lane group (GS-aligned in the wave), every lane gets it:
+// DPP xor 1 / xor 2 (quad_perm), row_half_mirror (8), row_mirror (16) inside a
+// row, ds_swizzle xor 16 across the two rows of a 32-lane half, and for
+// GS = 64 the two halves' values by readlane.  maxNum is exact and order-free,
+// so any tree gives the same value.  (Five __shfl_xor levels -- a
+// ds_bpermute round trip each, in the CFL loop's critical path every step --
+// took cfg 4 CFL 0.466 ms.)
+constexpr int kDppRowMirror = 0x140;
+constexpr int kDppRowHalfMirror = 0x141;
+
 template <int GS, typename T>
 __device__ __forceinline__ T group_max_abs(T m) {
-#pragma unroll
-  for (int off = GS / 2; off >= 1; off >>= 1) {
-    const T o = __shfl_xor(m, off, 64);
-    m = __builtin_fmax(o, m);  // (max_abs here measured slower: cfg 4 CFL 0.47 -> 0.51 ms)
-  }
+  static_assert(GS == 16 || GS == 32 || GS == 64, "Burgers groups are 16, 32 or 64 lanes");
+  m = max_of(m, dpp<qperm(1, 0, 3, 2)>(m));
+  m = max_of(m, dpp<qperm(2, 3, 0, 1)>(m));
+  m = max_of(m, dpp<kDppRowHalfMirror>(m));
+  m = max_of(m, dpp<kDppRowMirror>(m));
+  if constexpr (GS >= 32) m = max_of(m, swz_xor16(m));
+  if constexpr (GS == 64) m = max_of(__shfl(m, 0, 64), __shfl(m, 32, 64));
   return m;
 }
 
