@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 2 (r2ah): re-entry check on a rebuilt tree (container re-created):
+# the whole GPU parity suite, smoke, the bench line and rocprofv3 statistics
+# of the bench command.
+cd "$GRAFT_REPO_ROOT" || exit 2
+export TMPDIR=/tmp
+tools/gpu_session.sh \
+  "pytest_gpu:900:python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread -rf" \
+  "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "bench:300:python bench.py > gpurun_out/bench_line.json" \
+  "stats:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats -o run -- python bench.py --steps 20 --warmup 3 --no-cpu"
