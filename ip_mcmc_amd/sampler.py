@@ -337,13 +337,34 @@ class MCMCSampler:
         # one launch per sample: the whole loop (up to the next streaming flush)
         # in one ipmc_pcn_run call; consecutive sample slots are k elements apart
         blockwise = (not self.verbose) and 0 < sample_interval <= spl
+        # Large in-memory sample arrays go to the host in blocks of samples while
+        # the later blocks are still sweeping (copy stream, rectangular D2H
+        # copies into the page-locked result): only the last block's copy is
+        # left after the sweeps.
+        out_bytes = n_chains * n_samples * k * 8
+        overlap = (blockwise and keep == "samples" and sink is None and n_samples >= 2
+                   and OVERLAP_COPY_MIN_BYTES <= out_bytes <= PINNED_MAX_BYTES)
+        bounds = [n_samples]
+        copies = []  # (first sample, end sample, event after its sweeps)
+        src64 = None
+        if overlap:
+            n_blk = min(n_samples, OVERLAP_COPY_BLOCKS)
+            bounds = [(j + 1) * n_samples // n_blk for j in range(n_blk)]
+            if td != torch.float64:
+                # f64 staging for the converted blocks, allocated before any sweep
+                # is queued so that no block still in use is handed back to us
+                src64 = torch.empty((n_chains, n_samples, k), dtype=torch.float64, device=device)
         i = 0
         while blockwise and i < n_samples:  # sampler.py:23-28
             slot = i % buf_len  # 0: segments end where the staging buffer is full
-            nb = min(n_samples - i, buf_len - slot)
+            nb = min(n_samples - i, buf_len - slot, next(b for b in bounds if b > i) - i)
             launch_blocks(nb, sample_interval, None if samples is None else samples[:, slot, :], sums)
             if sink is not None:
                 samples = writer.flush(i - slot, slot + nb)
+            if overlap:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(device))
+                copies.append((i, i + nb, ev))
             i += nb
         for i in range(0 if not blockwise else n_samples, n_samples):  # sampler.py:23-28
             if self.verbose:
@@ -368,6 +389,17 @@ class MCMCSampler:
         host_out = None
         if keep == "samples" and sink is None:
             host_out = _host_buffer(tuple(samples.shape))
+        if overlap:
+            copy_stream = torch.cuda.Stream(device=device)
+            src = samples if src64 is None else src64
+            pitch = n_samples * k * 8
+            with torch.cuda.stream(copy_stream):
+                for i0, i1, ev in copies:
+                    copy_stream.wait_event(ev)
+                    if src64 is not None:
+                        src64[:, i0:i1].copy_(samples[:, i0:i1])
+                    dev.copy_rows_d2h(host_out.data_ptr() + i0 * k * 8, pitch, src.data_ptr() + i0 * k * 8, pitch,
+                                      (i1 - i0) * k * 8, n_chains, copy_stream.cuda_stream)
         torch.cuda.synchronize(device)
         self.last_run_seconds = time.perf_counter() - t0
 
@@ -396,7 +428,8 @@ class MCMCSampler:
         if keep == "samples":
             if sink is not None:
                 return sink.close()
-            host_out.copy_(samples if samples.dtype == torch.float64 else samples.double())
+            if not overlap:
+                host_out.copy_(samples if samples.dtype == torch.float64 else samples.double())
             out = host_out.numpy()  # shares the page-locked buffer (kept alive by the array)
             return out[0] if single else out
         if keep == "moments":
@@ -452,6 +485,10 @@ def _check_resume(state, chain_offset, accept_kind):
 # page-locked host buffers up to this size; larger sample arrays use pageable
 # memory (or stream to disk with run(sample_file=...))
 PINNED_MAX_BYTES = 8 << 30
+# in-memory sample arrays of at least this many bytes are copied to the host in
+# OVERLAP_COPY_BLOCKS blocks of samples while the sweeps run (MCMCSampler.run)
+OVERLAP_COPY_MIN_BYTES = 64 << 20
+OVERLAP_COPY_BLOCKS = 8
 
 
 class _StreamingWriter:

@@ -110,3 +110,23 @@ def test_pcn_run_streams_to_a_file(dev, tmp_path):
     s2, _ = _sampler(op, y, 0.5, False)
     f = s2.run(u0, n_samples=23, burn_in=10, sample_interval=3, sample_file=str(tmp_path / "s.npy"), flush_every=5)
     assert np.array_equal(np.asarray(f), mem)
+
+
+@pytest.mark.parametrize("case", ["l96", "l96_seq", "l96_f32", "linear1", "burgers"])
+def test_overlapped_sample_copy(dev, case, monkeypatch):
+    """Large in-memory sample arrays go to the host in blocks of samples on a
+    copy stream while the later blocks sweep (rectangular D2H copies into the
+    page-locked result; f32 converted on the device first).  Forced on at a
+    small size here: the result equals the per-sample launch loop's, for an
+    uneven split (37 samples in 8 blocks) and a single chain."""
+    from ip_mcmc_amd import sampler as S
+
+    rng = np.random.default_rng(11)
+    op, y, gamma, n, skw = _case(case, rng)
+    u0 = 0.1 * rng.normal(size=(n, op.k)) if n > 1 else 0.1 * rng.normal(size=op.k)
+    kw = dict(n_samples=37, burn_in=7, sample_interval=4)
+    b = _run(op, y, gamma, False, u0, "samples", True, skw, **kw)
+    monkeypatch.setattr(S, "OVERLAP_COPY_MIN_BYTES", 0)
+    a = _run(op, y, gamma, False, u0, "samples", False, skw, **kw)
+    assert a[0].dtype == np.float64 and a[0].shape == b[0].shape
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
