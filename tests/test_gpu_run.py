@@ -45,9 +45,10 @@ def _case(case, rng):
     if case.startswith("linear"):
         op = LinearOperator(rng.normal(size=(3, 4)))
         return op, rng.normal(size=3), 0.5, (1 if case == "linear1" else 4096), {}
-    if case == "l63":
+    if case in ("l63", "l63_f32"):
         op = Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=40)
-        return op, op(np.zeros(3)) + 0.2 * rng.normal(size=6), 0.5, 64, {}
+        # fp32: two speculative slots per lane (v_pk_* pairs)
+        return op, op(np.zeros(3)) + 0.2 * rng.normal(size=6), 0.5, 64, ({"dtype": np.float32} if case == "l63_f32" else {})
     if case == "burgers":
         op = BurgersOperator(N=32, dt_mode="cfl", T=0.3)
         return op, op(np.zeros(3)) + 0.05 * rng.normal(size=5), 0.1, 16, {}
@@ -64,8 +65,8 @@ def _case(case, rng):
     return op, y, 0.2, 300, skw
 
 
-@pytest.mark.parametrize("case", ["linear1", "linear4096", "l96", "l96_var", "l96_seq", "l96_f32", "l63", "burgers",
-                                  "ts"])
+@pytest.mark.parametrize("case", ["linear1", "linear4096", "l96", "l96_var", "l96_seq", "l96_f32", "l63", "l63_f32",
+                                  "burgers", "ts"])
 @pytest.mark.parametrize("keep", ["samples", "moments"])
 def test_pcn_run_equals_per_sample_launches(dev, case, keep):
     """In-launch samples (ipmc_sweep.sample_every, several samples per launch
