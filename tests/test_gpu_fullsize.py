@@ -84,3 +84,36 @@ def test_cfg4_full_ensemble_and_shards(dev, orc, dtype):
                           chain_offset=int(i))
         assert np.array_equal(full["u"][i], o["u"][0]) and full["acc"][i] == o["acc"][0], (dtype, i)
         assert full["phi"][i] == o["phi"][0], (dtype, i)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_headline_samples_overlapped_copy(dev, dtype, monkeypatch):
+    """MCMCSampler.run at the headline size (65 536 chains, d=40, 2 000 RK4
+    steps, 20 samples = 420 MB of f64 samples): the samples go to the host in
+    blocks while later blocks sweep (rectangular D2H at the real pitch).  The
+    result equals the run with one copy at the end, and its last sample is the
+    chains' final state."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, Lorenz96Operator,
+                             MCMCSampler, PhiloxRNG, pCNAccepter)
+    from ip_mcmc_amd import sampler as S
+
+    d, C_ = 40, 65536
+    op = Lorenz96Operator(d, 8.0, dt=0.005, n_steps=2000)
+    rng = np.random.default_rng(8)
+    y = op(np.zeros(d)) + 0.1 * rng.normal(size=d)
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(d), 0.01 * np.eye(d)))
+    prior = GaussianDistribution(np.zeros(d), np.eye(d))
+    u0 = 0.05 * rng.normal(size=(C_, d))
+
+    def run():
+        s = MCMCSampler(ConstSteppCNProposer(0.2, prior), pCNAccepter(pot), PhiloxRNG(4), dtype=dtype)
+        out = s.run(u0, n_samples=20, burn_in=1, sample_interval=1)
+        return out, s.state.u
+
+    assert C_ * 20 * d * 8 >= S.OVERLAP_COPY_MIN_BYTES  # the default path overlaps
+    a, ua = run()
+    monkeypatch.setattr(S, "OVERLAP_COPY_MIN_BYTES", 1 << 62)
+    b, _ = run()
+    assert a.shape == (C_, 20, d) and a.dtype == np.float64
+    assert np.array_equal(a, b)
+    assert np.array_equal(a[:, -1, :], np.asarray(ua, dtype=np.float64))
