@@ -194,7 +194,10 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
 // discarded and redone from the new state), so u, Φ, the counters, the sums
 // and the samples are bit-identical to the one-lane kernel; a round advances
 // the chain by up to S steps in one forward-map latency.
-constexpr int kSpecBlock = 256;
+#ifndef IPMC_SPEC_BLOCK  // block-size experiments (tools/build_variant.sh)
+#define IPMC_SPEC_BLOCK 256
+#endif
+constexpr int kSpecBlock = IPMC_SPEC_BLOCK;
 constexpr int kSpecKMax = 8;
 // linear G: A [q, k], y [q] and 1/γ [q] staged in LDS when q (k + 2) fits
 constexpr int kSpecLinLds = 1024;
