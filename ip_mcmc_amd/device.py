@@ -77,6 +77,16 @@ def _hip_runtime():
     return _hip
 
 
+def rect_copy_available():
+    """True when the HIP runtime's hipMemcpy2DAsync can be bound (the sampler
+    otherwise copies its samples in one piece after the sweeps)."""
+    try:
+        _hip_runtime()
+        return True
+    except (OSError, AttributeError):
+        return False
+
+
 def copy_rows_d2h(dst, dst_pitch, src, src_pitch, width, rows, stream):
     """Asynchronous rectangular copy device -> (page-locked) host on `stream`:
     `rows` rows of `width` bytes, row r from src + r*src_pitch to

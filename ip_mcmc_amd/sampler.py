@@ -343,7 +343,7 @@ class MCMCSampler:
         # left after the sweeps.
         out_bytes = n_chains * n_samples * k * 8
         overlap = (blockwise and keep == "samples" and sink is None and n_samples >= 2
-                   and OVERLAP_COPY_MIN_BYTES <= out_bytes <= PINNED_MAX_BYTES)
+                   and OVERLAP_COPY_MIN_BYTES <= out_bytes <= PINNED_MAX_BYTES and dev.rect_copy_available())
         bounds = [n_samples]
         copies = []  # (first sample, end sample, event after its sweeps)
         src64 = None
