@@ -1,15 +1,22 @@
 """Headline benchmark: pCN steps/s on Lorenz-96 d=40, 2000 RK4 steps, 65 536 chains.
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: launched by torch.distributed.run, one process per GPU)
+  (N > 1: started once, it launches torch.distributed.run with N ranks itself;
+   under an external torch.distributed.run WORLD_SIZE must equal N)
 
-A "step" is one pCN sweep: every chain of the batch proposes, runs its
-forward map (2000 RK4 steps of Lorenz-96, d=40), evaluates Φ and accepts or
-rejects -- one launch of the fused libipmc kernel.  Each GPU owns 65 536
-chains (weak scaling; global chain ids rank*65536 + i), inputs resident in
-HBM before the timed region.  value = all chains of all ranks x K / max-rank
-wall time.  Arithmetic: float64 (the reference computes in float64); the
-float32 throughput of the same workload is reported in "extra".
+A "step" is one pCN step of every chain of the batch: propose, run the forward
+map (2000 RK4 steps of Lorenz-96, d=40), evaluate Φ, accept or reject -- the
+fused libipmc kernel.  The metric's 65 536 chains are split over the N GPUs
+(strong scaling, the default; global chain ids rank*65536/N + i); the weak
+number (65 536 chains per GPU) is carried in "extra" for N > 1.  When a GPU
+holds fewer chains than fill it, one launch runs several pCN steps
+(--steps-per-launch, auto), so the speculative sweep can fill the lanes;
+results are bit-identical to one step per launch.  Inputs are resident in HBM
+before the timed region.  value = all chains of all ranks x K / max-rank wall
+time.  Arithmetic: float64 with the FMA forward map (the reference computes in
+float64); "extra" carries float32, the REFERENCE-arith (no FMA, the
+reference's operation order) throughput, and MCMCSampler.run end to end
+(host u_0 in, samples back on the host).
 
 roofline: VALU-bound (no MFMA, no HBM traffic inside the RK loop). achieved =
 algorithmic FLOP per launch / average kernel time from HIP events on the
@@ -24,6 +31,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -59,8 +68,9 @@ def problem():
 
 
 class Workload:
-    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0, d=D, chains_per_lane=0):
+    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0, d=D, chains_per_lane=0, per_launch=1):
         self.dev, self.dtype = dev, dtype
+        self.n_chains, self.per_launch = n_chains, per_launch
         self.model, self._keep = op.model(dtype, dev)
         t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
         self.y, self.ginv, self.sq = t(y), t(np.full(d, 1 / GAMMA)), t(np.ones(d))
@@ -77,14 +87,21 @@ class Workload:
         s.u, s.phi, s.accepts = self.u.data_ptr(), self.phi.data_ptr(), self.acc.data_ptr()
         s.y, s.gamma_inv, s.prior_sqrt = self.y.data_ptr(), self.ginv.data_ptr(), self.sq.data_ptr()
         s.beta, s.contraction = BETA, float(np.sqrt(1 - BETA**2))
-        s.seed, s.step0, s.n_steps = 2, 0, 1
+        s.seed, s.step0, s.n_steps = 2, 0, per_launch
         self.s = s
         # the plan the sweep runs (ipmc_plan_sweep: same code path as the launch)
         self.lanes, self.chains_per_lane, self.spec_width = sweep_plan(self.model, s)
 
-    def step(self):
+    def launches(self, n_steps):
+        """Launch sizes covering exactly n_steps pCN steps."""
+        full, rem = divmod(n_steps, self.per_launch)
+        return [self.per_launch] * full + ([rem] if rem else [])
+
+    def step(self, n=1):
+        """One launch of n pCN steps for every chain."""
+        self.s.n_steps = n
         call("ipmc_pcn_sweep", C.byref(self.model), C.byref(self.s), self.stream)
-        self.s.step0 += 1
+        self.s.step0 += n
 
 
 def sweep_plan(model, sweep):
@@ -121,28 +138,38 @@ def barrier(world):
         dist.barrier()
 
 
+def max_over_ranks(x, world, dev):
+    if world > 1:
+        t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        x = float(t.item())
+    return x
+
+
 def timed(w, steps, warmup, world):
-    for _ in range(warmup):
-        w.step()
+    """Exactly `steps` pCN steps of every chain (after `warmup` untimed ones),
+    bracketed by barrier + synchronize; (max-rank wall seconds, mean kernel ms
+    per full launch of w.per_launch steps, from HIP events on the launch stream)."""
+    for n in w.launches(warmup):
+        w.step(n)
     torch.cuda.synchronize(w.dev)
     barrier(world)
     torch.cuda.synchronize(w.dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    sizes = w.launches(steps)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in sizes]
     t0 = time.perf_counter()
-    for a, b in ev:
+    for (a, b), n in zip(ev, sizes):
         a.record()
-        w.step()
+        w.step(n)
         b.record()
     torch.cuda.synchronize(w.dev)
     barrier(world)
     torch.cuda.synchronize(w.dev)
     el = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=w.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    return el, kern_ms
+    full = [a.elapsed_time(b) for (a, b), n in zip(ev, sizes) if n == w.per_launch] or \
+           [a.elapsed_time(b) * w.per_launch / n for (a, b), n in zip(ev, sizes)]
+    kern_ms = float(np.mean(full))
+    return max_over_ranks(el, world, w.dev), kern_ms
 
 
 def cpu_baseline(op, y, dtype_np, budget_s=15.0):
@@ -175,14 +202,74 @@ def cpu_baseline(op, y, dtype_np, budget_s=15.0):
                       f"{'f64' if dtype_np == np.float64 else 'f32'}), C oracle, {threads} threads, {el:.1f} s"}
 
 
+def _free_port():
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run N ranks under
+    torch.distributed.run as a child process (nothing here has touched the GPU)
+    and relay its exit code; its rank 0 prints the line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {n} ranks: {' '.join(cmd)}")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def auto_per_launch(chains_per_rank):
+    """pCN steps per launch: 1 when the rank's chains fill the GPU (65 536
+    lanes at 1 chain per lane group), more when they do not, so the sweep can
+    speculate over the steps of a launch (ipmc_plan_sweep)."""
+    return int(max(1, min(64, CHAINS_PER_GPU // max(1, chains_per_rank))))
+
+
+def e2e_run(op, y, n_chains, chain_offset, dtype_np, dev, world, n_samples=20):
+    """MCMCSampler.run end to end (SURVEY §8(d)'s timed region): host u_0
+    (n_chains x 40) in, n_samples samples 1 step apart back on the host
+    (page-locked, copied in blocks while later blocks sweep)."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, MCMCSampler,
+                             PhiloxRNG, pCNAccepter)
+
+    prior = GaussianDistribution(np.zeros(D), np.eye(D))
+    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(D), GAMMA**2 * np.eye(D)))
+    u0 = np.zeros((n_chains, D))
+    s = MCMCSampler(ConstSteppCNProposer(BETA, prior), pCNAccepter(pot), PhiloxRNG(2), dtype=dtype_np, device=dev,
+                    chain_offset=chain_offset)
+    s.run(u0, n_samples=2, burn_in=1, sample_interval=1)  # warm: allocations, page-locked pool
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    t0 = time.perf_counter()
+    out = s.run(u0, n_samples=n_samples, burn_in=1, sample_interval=1)
+    el = time.perf_counter() - t0
+    assert out.shape == (n_chains, n_samples, D)
+    barrier(world)
+    el_max = max_over_ranks(el, world, dev)
+    tm = s.last_run_timing
+    return {"pcn_steps_per_s": world * n_chains * n_samples / el_max, "wall_s": el_max, "samples": n_samples,
+            "sample_bytes_per_rank": int(out.nbytes), "setup_ms": tm["setup_s"] * 1e3,
+            "sweeps_gpu_ms": tm["sweeps_gpu_ms"], "tail_ms_after_sweeps": tm["tail_ms"],
+            "copy_overlapped": tm["copy_overlapped"],
+            "note": "MCMCSampler.run(u0 host (chains x 40), n_samples, burn_in=1, sample_interval=1): H2D of u0, "
+                    "Phi(u0), the sweeps, D2H of the (chains, n_samples, 40) f64 samples; tail = wall after set-up "
+                    "not covered by the GPU sweeps (launch gaps + the last copy block + epilogue)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=CHAINS_PER_GPU, help="chains per GPU (weak) or in total (strong)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: --chains per GPU (default); strong: --chains split over the GPUs")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--chains", type=int, default=CHAINS_PER_GPU,
+                    help="total chains (strong, the default) or chains per GPU (weak)")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong: --chains split over the GPUs (the metric's 65 536; default); "
+                         "weak: --chains per GPU")
+    ap.add_argument("--steps-per-launch", type=int, default=0, help="pCN steps per kernel launch (0 = auto)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -193,11 +280,18 @@ def main():
                     help="every rank on cuda:0 (rehearsing N ranks on a one-GPU box; needs --dist-backend gloo)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.share_device and args.dist_backend != "gloo":
         raise SystemExit("--share-device needs --dist-backend gloo (RCCL wants one GPU per rank)")
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", 0 if args.share_device else local)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -208,17 +302,18 @@ def main():
 
     log(f"rank {rank}/{world} on {dev}: building the problem")
     op, y = problem()
-    if args.scaling == "strong":
-        if args.chains % world:
-            raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
-        args.chains //= world  # chains per rank from here on
+    total_chains = args.chains * (world if args.scaling == "weak" else 1)
+    if total_chains % world:
+        raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
+    per_rank = total_chains // world
+    per_launch = args.steps_per_launch or auto_per_launch(per_rank)
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
-    w = Workload(op, y, args.chains, rank * args.chains, tdt, dev, args.lanes)
-    log(f"timing {args.steps} sweeps ({args.dtype}, {args.chains} chains/GPU, lanes={w.lanes})")
+    w = Workload(op, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch)
+    log(f"timing {args.steps} pCN steps ({args.dtype}, {per_rank} chains/GPU, {per_launch} steps/launch, "
+        f"lanes={w.lanes}, spec_width={w.spec_width})")
     el, kern_ms = timed(w, args.steps, args.warmup, world)
     log(f"{args.dtype}: {el:.3f} s, kernel {kern_ms:.3f} ms/launch")
-    total_steps = world * args.chains * args.steps
-    value = total_steps / el
+    value = total_chains * args.steps / el
 
     # final gather of the per-chain results (the path's one exchange): accept
     # rate and posterior-mean state over all chains of all ranks
@@ -230,9 +325,9 @@ def main():
     barrier(world)
     tg = time.perf_counter()
     host = (lambda t: t.cpu()) if args.dist_backend == "gloo" else (lambda t: t)
-    u_all = gather_chains(host(w.u), world * args.chains)
-    phi_all = gather_chains(host(w.phi.view(-1, 1)), world * args.chains)
-    acc_all = gather_chains(host(w.acc.view(-1, 1)), world * args.chains)
+    u_all = gather_chains(host(w.u), total_chains)
+    phi_all = gather_chains(host(w.phi.view(-1, 1)), total_chains)
+    acc_all = gather_chains(host(w.acc.view(-1, 1)), total_chains)
     torch.cuda.synchronize(w.dev)
     gather_ms = (time.perf_counter() - tg) * 1e3
     gather = {"ms": gather_ms, "bytes_per_rank": int(w.u.numel() * w.u.element_size() + w.phi.numel() *
@@ -242,24 +337,45 @@ def main():
               "rows": int(u_all.shape[0])}
     assert bool(torch.isfinite(phi_all).all())
     del u_all, phi_all
-    accept_rate = float(acc_all.double().sum().item()) / (world * args.chains * (args.steps + args.warmup))
+    accept_rate = float(acc_all.double().sum().item()) / (total_chains * (args.steps + args.warmup))
 
     extra = {}
     if not args.no_extra:
+        xs = min(args.steps, 40)
         other = torch.float32 if tdt == torch.float64 else torch.float64
-        w2 = Workload(op, y, args.chains, rank * args.chains, other, dev, args.lanes)
-        el2, k2 = timed(w2, args.steps, args.warmup, world)
-        log(f"{other}: kernel {k2:.3f} ms/launch")
         key = "f32" if other == torch.float32 else "f64"
-        extra[f"{key}_pcn_steps_per_s"] = world * args.chains * args.steps / el2
+        w2 = Workload(op, y, per_rank, rank * per_rank, other, dev, args.lanes, per_launch=per_launch)
+        el2, k2 = timed(w2, xs, 2, world)
+        log(f"{key}: kernel {k2:.3f} ms/launch")
+        extra[f"{key}_pcn_steps_per_s"] = total_chains * xs / el2
         extra[f"{key}_kernel_ms"] = k2
-        extra[f"{key}_tflops"] = args.chains * FLOP_PER_STEP / (k2 * 1e-3) / 1e12
+        extra[f"{key}_tflops"] = per_rank * per_launch * FLOP_PER_STEP / (k2 * 1e-3) / 1e12
         del w2
+        # the reference's operation order (no FMA in the forward map): the
+        # arithmetic whose accept streams are pinned to the reference fixtures
+        op_ref = Lorenz96Operator(D, forcing_mean=8.0, x0=op.x0, dt=DT, n_steps=N_RK, arith="reference")
+        w3 = Workload(op_ref, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch)
+        el3, k3 = timed(w3, min(xs, 20), 2, world)
+        log(f"reference arith ({args.dtype}): kernel {k3:.3f} ms/launch")
+        extra["reference_arith_pcn_steps_per_s"] = total_chains * min(xs, 20) / el3
+        extra["reference_arith_kernel_ms"] = k3
+        extra["reference_arith_tflops"] = per_rank * per_launch * FLOP_PER_STEP / (k3 * 1e-3) / 1e12
+        del w3
+        if world > 1:  # weak scaling beside the strong line: 65 536 chains per GPU
+            w4 = Workload(op, y, CHAINS_PER_GPU, rank * CHAINS_PER_GPU, tdt, dev, args.lanes, per_launch=1)
+            el4, k4 = timed(w4, xs, 2, world)
+            extra["weak_scaling"] = {"pcn_steps_per_s": world * CHAINS_PER_GPU * xs / el4,
+                                     "total_chains": world * CHAINS_PER_GPU, "ms_per_step": el4 / xs * 1e3,
+                                     "kernel_ms": k4, "steps": xs}
+            del w4
+        extra["run_e2e"] = e2e_run(op, y, per_rank, rank * per_rank, np.float64 if tdt == torch.float64
+                                   else np.float32, dev, world)
+        extra["run_e2e_pcn_steps_per_s"] = extra["run_e2e"]["pcn_steps_per_s"]
 
-    flop = args.chains * FLOP_PER_STEP
+    flop = per_rank * per_launch * FLOP_PER_STEP
     achieved = flop / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    pmc, pmc_src = pmc_record(args.dtype, args.chains, w.lanes)
+    pmc, pmc_src = pmc_record(args.dtype, per_rank, w.lanes) if per_launch == 1 else (None, None)
     traffic = None if pmc is None else pmc["hbm_bytes_per_launch"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -285,17 +401,18 @@ def main():
             "data": "synthetic (forcing-field inverse problem, y = G(u_true) + N(0, 0.1^2), seed 3)",
             "config": {
                 "workload": "lorenz96_d40_rk4_2000_pcn",
-                "chains_per_gpu": args.chains,
-                "total_chains": world * args.chains,
+                "chains_per_gpu": per_rank,
+                "total_chains": total_chains,
                 "d": D,
                 "rk4_steps": N_RK,
                 "dt": DT,
                 "beta": BETA,
                 "arith": "fma",
+                "steps_per_launch": per_launch,
                 "lanes_per_chain": w.lanes,
                 "chains_per_lane": w.chains_per_lane,
                 "spec_width": w.spec_width,
-                "parallelism": f"chains sharded over {world} GPU(s)",
+                "parallelism": f"{total_chains} chains sharded over {world} GPU(s) ({args.scaling} scaling)",
             },
             "roofline": {
                 "bound": "valu",
@@ -306,7 +423,7 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC)",
                 "traffic_source": pmc_src,
-                "algorithmic_bytes": args.chains * (D * ITEM[args.dtype] + 2 * (ITEM[args.dtype] + 8)),
+                "algorithmic_bytes": per_rank * per_launch * (D * ITEM[args.dtype] + 2 * (ITEM[args.dtype] + 8)),
                 "hbm_GBps": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9,
                 "hbm_frac": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "kernel_ms": kern_ms,
@@ -325,7 +442,7 @@ def main():
             "final_gather": gather,
             "extra": extra,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

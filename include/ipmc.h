@@ -19,6 +19,10 @@
  *                                     stuart_examples.py:69-70,
  *                                     burgers/utilities.py:40-41
  *   GaussianDistribution.sample       distribution.py:114-118 ipmc_normal (counter-based N(0,I))
+ *   MCMCSampler._step with a Python G / constraint / noise model
+ *                                     sampler.py:35-41,       ipmc_pcn_draws (a block of steps' w and log r
+ *                                     potential.py:48-54,     for the host-side step; G runs in the caller)
+ *                                     accepter.py:39-62
  *   ConstStep/VarStepStandardRWProposer proposer.py:14-56     ipmc_sweep.proposal = IPMC_PROPOSAL_RW
  *   StandardRWAccepter._I             accepter.py:104-106     ipmc_sweep.reg_scale, ipmc_init_phi
  *   Lorenz96.__call__ (J > 0) + moment_function
@@ -54,7 +58,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 9
+#define IPMC_ABI_VERSION 10
 
 typedef enum {
   IPMC_OK = 0,
@@ -166,7 +170,10 @@ typedef struct ipmc_sweep {
                                sample_out + ((j+1)/sample_every - 1)*sample_step_stride (+ chain*sample_stride);
                                nothing else is written.  One launch then covers many samples and the speculative
                                sweeps run across sample boundaries. */
-  int64_t sample_step_stride; /* elements between consecutive samples of one chain (>= k when sample_every > 0) */
+  int64_t sample_step_stride; /* elements between consecutive samples of one chain (>= k when sample_every > 0);
+                                 with n_s = n_steps / sample_every samples per chain the rows may not overlap:
+                                 sample_stride >= (n_s-1)*sample_step_stride + k ([chain, sample, k]) or
+                                 sample_step_stride >= (n_chains-1)*sample_stride + k ([sample, chain, k]) */
 } ipmc_sweep;
 
 /* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */
@@ -203,6 +210,22 @@ int ipmc_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t 
 /* The accept uniforms: out[c] = r(seed, chain_offset + c, step) in [0,1), always double. */
 int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out,
                  void* stream);
+
+/* The random inputs of n_steps pCN steps for a HOST-side step (MCMCSampler.run with a Python forward map,
+   constraint predicate or noise model, sampler.py:35-41): for step s in [0, n_steps) (global pCN step
+   step0 + s) and chain c, w[(s*n_chains + c)*k + j] = the proposal noise exactly as the sweep kernels form
+   it -- prior_sqrt[j] * xi_j, or sum_{i<=j} prior_chol[j][i] * xi_i in ascending i from +0 (no FMA) --
+   in dtype, and, if log_r is not NULL, log_r[s*n_chains + c] = log r with the kernels' deterministic log
+   (accept iff (double)(phi_u - phi_v) > log_r, accepter.py:62).  step0 + n_steps <= 2^63. */
+int ipmc_pcn_draws(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step0, int64_t n_steps,
+                   int32_t k, int32_t dtype, const void* prior_sqrt, const void* prior_chol, void* w,
+                   double* log_r, void* stream);
+
+/* Asynchronous rectangular copy device -> host (page-locked for overlap) on `stream`: `rows` rows of
+   `width` bytes, row r from src + r*src_pitch to dst + r*dst_pitch (the sampler's block-wise sample
+   copy; inside libipmc so that it runs on the HIP runtime the caller's stream belongs to). */
+int ipmc_copy_rows_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t width,
+                       int64_t rows, void* stream);
 
 /* Batched normalised autocorrelation (MCMCSampler.autocorr, sampler.py:43-54):
    series s is x[s*stride_series + t*stride_t], t < len (any len; series over 8192 samples stream through LDS tiles);

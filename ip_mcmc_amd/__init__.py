@@ -34,12 +34,17 @@ from .forward import (
     TwoScaleLorenz96Operator,
 )
 from .rng import PhiloxRNG, PhiloxStream
+
+# the name report/scripts/stuart_examples.py:6 imports (the package's
+# ConstSteppCNProposer under its older name)
+pCNProposer = ConstSteppCNProposer
 from ._lib import IpmcError, UnsupportedOnDevice
 
 __all__ = [
     "MCMCSampler",
     "ProposerBase",
     "ConstSteppCNProposer",
+    "pCNProposer",
     "VarSteppCNProposer",
     "ConstStepStandardRWProposer",
     "VarStepStandardRWProposer",

@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -113,6 +113,13 @@ SIGNATURES = {
         [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p],
     ),
     "ipmc_uniform": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "ipmc_pcn_draws": (
+        C.c_int,
+        [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+         C.c_void_p, C.c_void_p, C.c_void_p],
+    ),
+    "ipmc_copy_rows_d2h": (
+        C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p]),
     "ipmc_autocorr": (
         C.c_int,
         [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p],

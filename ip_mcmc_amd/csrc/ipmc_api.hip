@@ -2,6 +2,7 @@
 // choice and launch.  Small-state models (linear, Lorenz-63) and the RNG
 // probes live here; Lorenz-96 and Burgers in their own translation units.
 #include <stdarg.h>
+#include <algorithm>
 #include <stdio.h>
 
 #include "ipmc_internal.hpp"
@@ -304,6 +305,38 @@ __global__ void reg_add_kernel(int64_t n, int k, const T* __restrict__ u, const 
   phi[i] = phi[i] + small_regularizer<T, FM>(k, c, u + i * k, 1);
 }
 
+// ipmc_pcn_draws: one thread per (step, chain, component), grid-stride.  w is
+// formed with pcn_propose's / chol_propose's operations (the same bits as the
+// sweep kernels' proposal noise); the j = 0 thread also writes log r.
+template <typename T>
+__global__ void draws_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t step0, int64_t total, int k,
+                             const T* __restrict__ sq, const T* __restrict__ chol, T* __restrict__ w,
+                             double* __restrict__ log_r) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sc = i / k;
+    const int j = (int)(i - sc * k);
+    const int64_t s = sc / n;
+    const uint64_t gid = (uint64_t)(c_off + (sc - s * n));
+    const uint64_t step = step0 + (uint64_t)s;
+    double z0, z1;
+    T wj;
+    if (chol) {
+      wj = (T)0;
+      for (int ii = 0; ii <= j; ii += 2) {
+        normal_pair(seed, gid, step, (uint32_t)(ii >> 1), z0, z1);
+        wj = wj + (T)z0 * chol[(int64_t)j * k + ii];
+        if (ii + 1 <= j) wj = wj + (T)z1 * chol[(int64_t)j * k + ii + 1];
+      }
+    } else {
+      normal_pair(seed, gid, step, (uint32_t)(j >> 1), z0, z1);
+      wj = sq[j] * (T)((j & 1) ? z1 : z0);
+    }
+    w[i] = wj;
+    if (j == 0 && log_r) log_r[sc] = det_log(accept_uniform(seed, gid, step));
+  }
+}
+
 __global__ void uniform_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t step, double* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -416,6 +449,18 @@ int ipmc_pcn_sweep(const ipmc_model* m, const ipmc_sweep* s, void* stream) {
     return fail(IPMC_ERR_INVALID, "sample_every must be in [0, 2^31)");
   if (s->sample_every > 0 && (!s->sample_out || s->sample_step_stride < m->k || s->sample_stride < m->k))
     return fail(IPMC_ERR_INVALID, "sample_every needs sample_out, sample_stride >= k and sample_step_stride >= k");
+  if (s->sample_every > 0 && s->n_chains > 1) {
+    // the n_s samples of a chain must not reach into another chain's rows
+    const int64_t ns = s->n_steps / s->sample_every;
+    if (ns > 0) {
+      const bool chain_major = (s->sample_stride - m->k) / s->sample_step_stride >= ns - 1;
+      const bool sample_major = (s->sample_step_stride - m->k) / s->sample_stride >= s->n_chains - 1;
+      if (!chain_major && !sample_major)
+        return fail(IPMC_ERR_INVALID,
+                    "sample_every: the samples overlap; need sample_stride >= (n_s-1)*sample_step_stride + k or "
+                    "sample_step_stride >= (n_chains-1)*sample_stride + k, n_s = n_steps / sample_every");
+    }
+  }
   if (s->n_chains == 0 || s->n_steps == 0) {
     if (s->n_chains > 0 && s->sample_out && s->sample_every == 0) {
       // no step: the sample is the current state
@@ -542,6 +587,46 @@ int ipmc_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t
   hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, seed, chain_offset,
                      n_chains, step, out);
   return check_launch("uniform_kernel");
+}
+
+int ipmc_pcn_draws(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step0, int64_t n_steps,
+                   int32_t k, int32_t dtype, const void* prior_sqrt, const void* prior_chol, void* w,
+                   double* log_r, void* stream) {
+  if (k <= 0 || n_steps < 0) return fail(IPMC_ERR_INVALID, "k must be positive and n_steps >= 0");
+  int rc = check_chain_range(chain_offset, n_chains);
+  if (rc) return rc;
+  if (dtype != IPMC_F32 && dtype != IPMC_F64) return fail(IPMC_ERR_INVALID, "bad dtype");
+  if (step0 > kHostStepBase || (uint64_t)n_steps > kHostStepBase - step0)
+    return fail(IPMC_ERR_INVALID, "pCN steps must stay below 2^63 (the host-draw range)");
+  if (n_chains == 0 || n_steps == 0) return IPMC_OK;
+  if (!w) return fail(IPMC_ERR_INVALID, "w is NULL");
+  if (!prior_sqrt && !prior_chol) return fail(IPMC_ERR_INVALID, "prior_sqrt and prior_chol are both NULL");
+  if (n_chains > INT64_MAX / k / n_steps) return fail(IPMC_ERR_INVALID, "n_steps * n_chains * k overflows");
+  const int64_t total = n_steps * n_chains * k;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == IPMC_F64)
+    hipLaunchKernelGGL(draws_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, st, seed, chain_offset, n_chains,
+                       step0, total, k, (const double*)prior_sqrt, (const double*)prior_chol, (double*)w, log_r);
+  else
+    hipLaunchKernelGGL(draws_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, st, seed, chain_offset, n_chains,
+                       step0, total, k, (const float*)prior_sqrt, (const float*)prior_chol, (float*)w, log_r);
+  return check_launch("draws_kernel");
+}
+
+int ipmc_copy_rows_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t width,
+                       int64_t rows, void* stream) {
+  if (rows < 0 || width < 0) return fail(IPMC_ERR_INVALID, "negative count");
+  if (rows == 0 || width == 0) return IPMC_OK;
+  if (!dst || !src) return fail(IPMC_ERR_INVALID, "dst / src is NULL");
+  if (dst_pitch < width || src_pitch < width) return fail(IPMC_ERR_INVALID, "pitch < width");
+  const hipError_t e = hipMemcpy2DAsync(dst, (size_t)dst_pitch, src, (size_t)src_pitch, (size_t)width,
+                                        (size_t)rows, hipMemcpyDeviceToHost, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    set_error("hipMemcpy2DAsync: %s", hipGetErrorString(e));
+    return IPMC_ERR_DEVICE;
+  }
+  return IPMC_OK;
 }
 
 }  // extern "C"

@@ -15,6 +15,9 @@
 
 namespace ipmc {
 
+// LDS per CU on gfx950 (MI355X): the static LDS of any block must fit this.
+constexpr size_t kLdsBytesPerCU = 160 * 1024;
+
 // ---------------------------------------------------------------- Philox
 struct u32x4 {
   uint32_t x, y, z, w;

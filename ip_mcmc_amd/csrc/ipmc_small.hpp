@@ -194,6 +194,8 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
 // discarded and redone from the new state), so u, Φ, the counters, the sums
 // and the samples are bit-identical to the one-lane kernel; a round advances
 // the chain by up to S steps in one forward-map latency.
+// gfx950 only: the f64 linear kernel's LDS (small_spec_lds_bytes) is 96 KiB at
+// the default 256 threads, static_assert'ed against kLdsBytesPerCU.
 #ifndef IPMC_SPEC_BLOCK  // block-size experiments (tools/build_variant.sh)
 #define IPMC_SPEC_BLOCK 256
 #endif
@@ -229,8 +231,21 @@ __device__ __forceinline__ T lin_potential_staged(const T* As, const T* ys, cons
 constexpr int kPreFactor = 4;
 constexpr int kPreLds = kPreFactor * kSpecBlock;  // steps per block (all groups)
 
+// LDS of one small_spec_kernel block: the proposal park, the linear model's
+// constants and (linear) the pre-drawn w / log r.  f64 at kSpecBlock = 256 is
+// 96 KiB -- it fits gfx950's 160 KiB per CU only (64 KiB on gfx942): a larger
+// IPMC_SPEC_BLOCK or kPreFactor has to stay under the limit.
+template <typename T, int MODEL>
+constexpr size_t small_spec_lds_bytes() {
+  return sizeof(T) * (size_t)kSpecKMax * kSpecBlock + sizeof(T) * (MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1) +
+         (MODEL == IPMC_MODEL_LINEAR ? (sizeof(T) * (size_t)kPreLds * kSpecKMax + sizeof(double) * kPreLds)
+                                     : sizeof(T) + sizeof(double));
+}
+
 template <typename T, int MODEL, bool FM, int S>
 __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model m, const ipmc_sweep s) {
+  static_assert(small_spec_lds_bytes<T, MODEL>() <= kLdsBytesPerCU,
+                "small_spec_kernel: LDS per block exceeds the CU's LDS (gfx950: 160 KiB)");
   constexpr bool PRE = (MODEL == IPMC_MODEL_LINEAR);
   constexpr int C = kPreFactor * S;  // steps of draws a group holds
   __shared__ T vpark[kSpecKMax * kSpecBlock];

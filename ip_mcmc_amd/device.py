@@ -4,8 +4,6 @@ thin wrappers over the libipmc entry points that are not the sweep itself.
 PyTorch is used only for memory, streams and torch.distributed; all compute is
 libipmc's HIP kernels.
 """
-import ctypes as C
-
 import numpy as np
 import torch
 
@@ -60,43 +58,20 @@ def to_device(x, dtype, device):
     return torch.as_tensor(np.asarray(x, dtype=np.float64), dtype=dtype).to(device).contiguous()
 
 
-_hip = None
-HIP_MEMCPY_DEVICE_TO_HOST = 2  # hipMemcpyKind
-
-
-def _hip_runtime():
-    """The HIP runtime torch has already loaded (dlopen by soname returns that
-    instance, the one libipmc and torch's streams use)."""
-    global _hip
-    if _hip is None:
-        h = C.CDLL("libamdhip64.so.7")
-        f = h.hipMemcpy2DAsync
-        f.restype = C.c_int
-        f.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int, C.c_void_p]
-        _hip = h
-    return _hip
-
-
 def rect_copy_available():
-    """True when the HIP runtime's hipMemcpy2DAsync can be bound (the sampler
-    otherwise copies its samples in one piece after the sweeps)."""
-    try:
-        _hip_runtime()
-        return True
-    except (OSError, AttributeError):
-        return False
+    """The block-wise sample copy goes through libipmc (ipmc_copy_rows_d2h),
+    which runs on the HIP runtime the caller's streams belong to: always
+    available once the library loads."""
+    return True
 
 
 def copy_rows_d2h(dst, dst_pitch, src, src_pitch, width, rows, stream):
     """Asynchronous rectangular copy device -> (page-locked) host on `stream`:
     `rows` rows of `width` bytes, row r from src + r*src_pitch to
-    dst + r*dst_pitch (hipMemcpy2DAsync)."""
+    dst + r*dst_pitch (ipmc_copy_rows_d2h = hipMemcpy2DAsync inside libipmc)."""
     if rows <= 0 or width <= 0:
         return
-    rc = _hip_runtime().hipMemcpy2DAsync(dst, dst_pitch, src, src_pitch, width, rows, HIP_MEMCPY_DEVICE_TO_HOST,
-                                         stream)
-    if rc != 0:
-        raise RuntimeError(f"hipMemcpy2DAsync failed with hipError {rc}")
+    call("ipmc_copy_rows_d2h", dst, dst_pitch, src, src_pitch, width, rows, stream)
 
 
 def normals(seed, chain_offset, n_chains, step, k, dtype=None, device=None):

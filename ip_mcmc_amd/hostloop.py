@@ -1,0 +1,495 @@
+"""Host-side pCN loop for compositions the fused kernels cannot run.
+
+The reference's plugin API takes any Python callable as the forward map
+(``EvolutionPotential(G, data, noise)``, potential.py:48-54; config 1's caller
+passes the closure ``G(u) = np.dot(g, u)``, stuart_examples.py:69-70), any
+predicate as a constraint (``ConstrainAccepter``, accepter.py:39-55), any
+Gaussian noise model and any proposer/accepter implementing its ABCs.  The
+fused sweep kernels run a fixed set of device forward maps; for everything else
+``MCMCSampler.run`` comes here.  This is not a CPU fallback for device
+compositions (those always take the kernels): it is the one place a caller's
+Python code has to run, and the GPU still supplies the randomness.
+
+Two tiers:
+
+* **Structured** (vectorised over the chains): a pCN / RW proposer with any
+  prior covariance, ``CountedAccepter`` / ``ConstrainAccepter`` layers in any
+  order, ``pCNAccepter`` or ``StandardRWAccepter`` (any prior), over an
+  ``EvolutionPotential`` with any G and any ``GaussianDistribution`` noise, or
+  over any other potential object.  Per block of steps one
+  ``ipmc_pcn_draws`` launch produces the proposal noise ``w`` (the sweep
+  kernels' own operations: ``sqrt(C_ii)·ξ_i`` or ``Σ_{i<=j} L_ji ξ_i``) and
+  ``log r`` (the kernels' deterministic log); the host forms
+  ``v = contraction·u + β·w`` (``u + β·w`` for RW) in the chain dtype,
+  evaluates the constraints and G, and accepts iff ``(double)(Φu − Φv) > log r``
+  -- the kernels' sequence of operations.  For a diagonal noise Φ is
+  ``½ Σ_i ((y_i − m_i − g_i)·γ_i⁻¹)²`` summed in component order without FMA,
+  so a device-expressible G run through this loop gives the fused kernel's
+  bits in REFERENCE arith.  A device ``ObservationOperator`` is evaluated in
+  one ``ipmc_forward`` launch per step for all chains; a Python G is called
+  once per chain and step, as the reference calls it.
+* **Generic** (any other proposer or accepter, e.g. a user subclass of
+  ``ProposerBase`` / ``AccepterBase``): the reference's own ``_step``
+  (sampler.py:35-41) per chain, with an rng whose ``multivariate_normal`` and
+  ``random`` return the same counter-based draws (the reference's MockRNG seam,
+  test_utilities.py:11-26).
+"""
+import numpy as np
+import torch
+
+from . import device as dev
+from ._lib import call
+from .accepter import ConstrainAccepter, CountedAccepter, StandardRWAccepter, pCNAccepter
+from .chainio import ChainState, NpySampleSink
+from .distribution import GaussianDistribution
+from .forward import ObservationOperator
+from .potential import EvolutionPotential
+
+# bytes of draws (w) fetched from the device per block of steps
+DRAW_BLOCK_BYTES = 64 << 20
+
+
+# ------------------------------------------------------------------ draws
+def device_draws(seed, chain_offset, n_chains, step0, n_steps, k, np_dtype, prior_sqrt, prior_chol, device=None):
+    """(w [n_steps, C, k] in np_dtype, log r [n_steps, C] float64) from
+    ipmc_pcn_draws on `device`."""
+    device = dev.resolve_device(device)
+    td = dev.torch_dtype(np_dtype)
+    sq = None if prior_sqrt is None else dev.to_device(prior_sqrt, td, device)
+    ch = None if prior_chol is None else dev.to_device(prior_chol, td, device)
+    w = torch.empty((n_steps, n_chains, k), dtype=td, device=device)
+    lr = torch.empty((n_steps, n_chains), dtype=torch.float64, device=device)
+    call("ipmc_pcn_draws", seed, chain_offset, n_chains, step0, n_steps, k, dev.abi_dtype(td), dev.ptr(sq),
+         dev.ptr(ch), w.data_ptr(), lr.data_ptr(), dev.stream_handle(device))
+    return w.cpu().numpy(), lr.cpu().numpy()
+
+
+def device_raw_draws(seed, chain_offset, n_chains, step0, n_steps, k, device=None):
+    """(ξ [n_steps, C, k], r [n_steps, C]) float64: ipmc_normal / ipmc_uniform on `device`."""
+    device = dev.resolve_device(device)
+    xi = torch.empty((n_steps, n_chains, k), dtype=torch.float64, device=device)
+    r = torch.empty((n_steps, n_chains), dtype=torch.float64, device=device)
+    st = dev.stream_handle(device)
+    for s in range(n_steps):
+        call("ipmc_normal", seed, chain_offset, n_chains, step0 + s, k, dev.abi_dtype(torch.float64),
+             xi[s].data_ptr(), st)
+        call("ipmc_uniform", seed, chain_offset, n_chains, step0 + s, r[s].data_ptr(), st)
+    return xi.cpu().numpy(), r.cpu().numpy()
+
+
+# the providers the loop uses (tests on a CPU-only machine substitute the
+# oracle's draws for these; the product path has no other source)
+DRAWS = {"w": device_draws, "raw": device_raw_draws}
+
+
+class GenericComposition(Exception):
+    """The composition is not in the structured tier's vocabulary."""
+
+
+# ------------------------------------------------------------- structured
+class HostPlan:
+    """The structured tier's reading of a proposer/accepter composition."""
+
+    def __init__(self, proposer, accepter, k):
+        kind = getattr(proposer, "kind", None)
+        prior = getattr(proposer, "w", None)
+        if kind not in ("pcn", "rw") or not isinstance(prior, GaussianDistribution):
+            raise GenericComposition(type(proposer).__name__)
+        if prior.k != k:
+            raise ValueError(f"prior dimension {prior.k} != state dimension {k}")
+        self.proposer = proposer
+        self.rw = kind == "rw"
+        if prior.is_diagonal:
+            self.prior_sqrt, self.prior_chol = prior.sqrt_diagonal, None
+        else:
+            self.prior_sqrt, self.prior_chol = None, prior.L
+        self.layers = []  # ("count", CountedAccepter) | ("constrain", predicate), outermost first
+        acc = accepter
+        while True:
+            if isinstance(acc, CountedAccepter):
+                self.layers.append(("count", acc))
+                acc = acc.accepter
+            elif isinstance(acc, ConstrainAccepter):
+                self.layers.append(("constrain", acc.is_valid))
+                acc = acc.accepter
+            elif isinstance(acc, pCNAccepter):
+                self.reg_prior = None
+                break
+            elif isinstance(acc, StandardRWAccepter):
+                self.reg_prior = acc.prior
+                break
+            else:
+                raise GenericComposition(type(acc).__name__)
+        self.potential = acc.theta
+        self.accept_kind = "pcn" if self.reg_prior is None else "rw_reg"
+
+
+class _Misfit:
+    """Φ for a stack of proposals, in the chain dtype T."""
+
+    def __init__(self, potential, T, device):
+        self.T, self.device = T, device
+        self.pot = potential
+        self.G = None
+        if isinstance(potential, EvolutionPotential) and isinstance(potential.rho, GaussianDistribution):
+            rho = potential.rho
+            self.G = potential.G
+            y_eff = np.atleast_1d(np.asarray(potential.y, dtype=np.float64)) - rho.mean
+            if rho.k != y_eff.shape[0]:
+                raise ValueError(f"data dimension {y_eff.shape[0]} != noise dimension {rho.k}")
+            self.diag = rho.is_diagonal
+            if self.diag:
+                # the kernels' misfit terms: y - m and 1/γ rounded to T
+                self.y_eff = y_eff.astype(T)
+                self.ginv = (1.0 / np.sqrt(rho.covariance_diagonal)).astype(T)
+            else:
+                self.y_eff64 = y_eff
+                self.Lg = rho.L
+
+    def forward(self, V):
+        """G for the rows of V (n, k) -> (n, q)."""
+        G = self.G
+        if isinstance(G, ObservationOperator):
+            td = dev.torch_dtype(self.T)
+            g = G.forward_device(dev.to_device(V, td, dev.resolve_device(self.device)), td)
+            return g.cpu().numpy()
+        rows = [np.atleast_1d(np.asarray(G(v), dtype=np.float64)).reshape(-1) for v in V.astype(np.float64)]
+        return np.stack(rows) if rows else np.zeros((0, 0))
+
+    def __call__(self, V):
+        T = self.T
+        n = V.shape[0]
+        if n == 0:
+            return np.zeros(0, dtype=T)
+        if self.G is None:  # any potential object: its own value (constant included)
+            return np.array([float(self.pot(v)) for v in V.astype(np.float64)], dtype=np.float64).astype(T)
+        g = self.forward(V)
+        if self.diag:
+            r = (self.y_eff[None, :] - g.astype(T)) * self.ginv[None, :]
+            s = np.zeros(n, dtype=T)
+            for i in range(r.shape[1]):  # component order, no FMA (REFERENCE arith's sum)
+                s = s + r[:, i] * r[:, i]
+            return T(0.5) * s
+        # dense noise Γ = L Lᵀ: ½‖L⁻¹(y − m − G)‖² (−logpdf without its constant)
+        from scipy.linalg import solve_triangular
+
+        z = solve_triangular(self.Lg, (self.y_eff64[None, :] - g.astype(np.float64)).T, lower=True)
+        return (0.5 * np.sum(z * z, axis=0)).astype(T)
+
+
+def _regularizer(prior, V, T):
+    """StandardRWAccepter's ½‖prior.apply_sqrt_covariance(v)‖² (accepter.py:104-106,
+    Q6): diagonal prior in the kernels' order, else through the Cholesky factor."""
+    if prior.is_diagonal:
+        c = prior.sqrt_diagonal.astype(T)
+        s = np.zeros(V.shape[0], dtype=T)
+        for j in range(V.shape[1]):
+            t = c[j] * V[:, j]
+            s = s + t * t
+        return T(0.5) * s
+    t = V.astype(np.float64) @ prior.L.T
+    return (0.5 * np.sum(t * t, axis=1)).astype(T)
+
+
+class _Recorder:
+    """Samples / moments / last state of a host run, like the device path's outputs."""
+
+    def __init__(self, keep, n_chains, n_samples, k, single, sample_file):
+        self.keep, self.single = keep, single
+        self.sink = None
+        self.samples = None
+        if keep == "samples":
+            if sample_file is not None:
+                self.sink = NpySampleSink(sample_file, (n_samples, k) if single else (n_chains, n_samples, k))
+            else:
+                self.samples = np.empty((n_chains, n_samples, k), dtype=np.float64)
+        self.sum_u = self.sum_u2 = None
+        if keep == "moments":
+            self.sum_u = np.zeros((n_chains, k), dtype=np.float64)
+            self.sum_u2 = np.zeros((n_chains, k), dtype=np.float64)
+
+    def record(self, i, u):
+        ud = u.astype(np.float64)
+        if self.sink is not None:
+            self.sink.write(i, ud[0][None, :] if self.single else ud[:, None, :])
+        elif self.samples is not None:
+            self.samples[:, i, :] = ud
+
+    def accumulate(self, u):
+        if self.sum_u is not None:
+            ud = u.astype(np.float64)
+            self.sum_u += ud
+            self.sum_u2 += ud * ud
+
+
+def _schedule(plan, i0, n, T):
+    """(beta, contraction) of proposals i0+1 .. i0+n as T, per step."""
+    p = plan.proposer
+    if hasattr(p, "device_step"):
+        b, c = p.device_step()
+        return np.full(n, b, dtype=np.float64).astype(T), np.full(n, c, dtype=np.float64).astype(T)
+    sched = p.beta_schedule(i0, n)
+    return sched[:, 0].astype(T), sched[:, 1].astype(T)
+
+
+def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_samples, interval, rec, device):
+    """Advance the chains (U [C, k] and Φ(U) [C], both dtype T, updated in
+    place) by n_burn steps, then n_samples blocks of `interval` steps recording
+    the state after each block (sampler.py:18-28).  Returns (accepts, calls per
+    count layer, steps run)."""
+    T = U.dtype.type
+    C_, k = U.shape
+    misfit = _Misfit(plan.potential, T, device)
+    counts = [np.zeros(C_, dtype=np.int64) for lay in plan.layers if lay[0] == "count"]
+    acc_total = np.zeros(C_, dtype=np.int64)
+    total = n_burn + n_samples * interval
+    block = max(1, min(total, DRAW_BLOCK_BYTES // max(1, C_ * k * U.itemsize)))
+    done = 0
+    post = 0  # post-burn-in steps done
+    while done < total:
+        nb = min(block, total - done)
+        w, log_r = DRAWS["w"](seed, chain_offset, C_, step + done, nb, k, T, plan.prior_sqrt, plan.prior_chol,
+                              device)
+        betas, contrs = _schedule(plan, prop_i + done, nb, T)
+        for s in range(nb):
+            V = U + betas[s] * w[s] if plan.rw else contrs[s] * U + betas[s] * w[s]
+            reach = np.ones(C_, dtype=bool)
+            reached = []
+            for kind, obj in plan.layers:
+                if kind == "count":
+                    reached.append(reach.copy())
+                else:
+                    idx = np.flatnonzero(reach)
+                    if idx.size:
+                        ok = np.array([bool(obj(V[c])) for c in idx], dtype=bool)
+                        reach[idx[~ok]] = False
+            idx = np.flatnonzero(reach)
+            accepted = np.zeros(C_, dtype=bool)
+            if idx.size:
+                Vi = V[idx]
+                phv = misfit(Vi)
+                if plan.reg_prior is not None:
+                    phv = phv + _regularizer(plan.reg_prior, Vi, T)
+                a = (phi[idx] - phv).astype(np.float64) > log_r[s, idx]
+                sel = idx[a]
+                U[sel] = Vi[a]
+                phi[sel] = phv[a]
+                accepted[sel] = True
+            acc_total += accepted
+            for ci, r in enumerate(reached):
+                counts[ci] += r
+            if done + s >= n_burn:
+                rec.accumulate(U)
+                post += 1
+                if post % interval == 0:
+                    rec.record(post // interval - 1, U)
+        done += nb
+    return acc_total, counts, total
+
+
+def initial_phi(plan, U, device):
+    T = U.dtype.type
+    phi = _Misfit(plan.potential, T, device)(U)
+    if plan.reg_prior is not None:
+        phi = phi + _regularizer(plan.reg_prior, U, T)
+    return phi
+
+
+# ----------------------------------------------------------------- generic
+class StepRNG:
+    """The rng handed to a caller's proposer/accepter in the generic tier: the
+    draws of one (chain, step), like the reference's MockRNG seam
+    (test_utilities.py:11-26).  multivariate_normal(mean, cov) = mean + sqrt(C)·ξ
+    (diagonal C) or mean + L·ξ in the kernels' order; random() = r."""
+
+    def __init__(self):
+        self.xi = None
+        self.r = None
+
+    def set(self, xi, r):
+        self.xi, self.r = xi, r
+
+    def multivariate_normal(self, mean=None, cov=None):
+        mean = np.atleast_1d(np.asarray(mean, dtype=np.float64))
+        k = mean.shape[0]
+        if k > self.xi.shape[0]:
+            raise ValueError(f"draw of dimension {k} > the chain's {self.xi.shape[0]}")
+        xi = self.xi[:k]
+        cov = np.asarray(cov, dtype=np.float64).reshape(k, k)
+        if np.all(cov == np.diag(np.diag(cov))):
+            return np.sqrt(np.diag(cov)) * xi + mean
+        L = np.linalg.cholesky(cov)
+        w = np.zeros(k)
+        for j in range(k):
+            a = 0.0
+            for i in range(j + 1):
+                a = a + float(xi[i]) * float(L[j, i])
+            w[j] = a
+        return w + mean
+
+    def random(self):
+        return float(self.r)
+
+
+def _counted(acc):
+    """Every CountedAccepter reachable through .accepter attributes."""
+    out = []
+    seen = set()
+    while acc is not None and id(acc) not in seen:
+        seen.add(id(acc))
+        if isinstance(acc, CountedAccepter):
+            out.append(acc)
+        acc = getattr(acc, "accepter", None)
+    return out
+
+
+def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_samples, interval, rec, device):
+    """The reference's _step (sampler.py:35-41) per chain with StepRNG draws.
+    Returns per-chain (calls, accepts) of every CountedAccepter found."""
+    C_, k = U.shape
+    total = n_burn + n_samples * interval
+    counted = _counted(accepter)
+    per = {id(ca): (np.zeros(C_, dtype=np.int64), np.zeros(C_, dtype=np.int64)) for ca in counted}
+    rng = StepRNG()
+    block = max(1, min(total, DRAW_BLOCK_BYTES // max(1, C_ * k * 8)))
+    u_rows = [np.asarray(U[c], dtype=np.float64).copy() for c in range(C_)]
+    done = 0
+    post = 0
+    while done < total:
+        nb = min(block, total - done)
+        xi, r = DRAWS["raw"](seed, chain_offset, C_, step + done, nb, k, device)
+        for s in range(nb):
+            for c in range(C_):
+                before = [(ca.calls, ca.accepts) for ca in counted]
+                rng.set(xi[s, c], r[s, c])
+                v = proposer(u_rows[c], rng)
+                if accepter(u_rows[c], v, rng):
+                    u_rows[c] = np.asarray(v, dtype=np.float64)
+                for ca, (c0, a0) in zip(counted, before):
+                    per[id(ca)][0][c] += int(np.sum(ca.calls)) - int(np.sum(c0))
+                    per[id(ca)][1][c] += int(np.sum(ca.accepts)) - int(np.sum(a0))
+            if done + s >= n_burn:
+                Ucur = np.stack(u_rows)
+                rec.accumulate(Ucur)
+                post += 1
+                if post % interval == 0:
+                    rec.record(post // interval - 1, Ucur)
+        done += nb
+    U[:] = np.stack(u_rows).astype(U.dtype) if C_ else U
+    return counted, per, total
+
+
+# --------------------------------------------------------------------- run
+def run(sampler, u_0, n_samples, burn_in, sample_interval, keep, sample_file, reason):
+    """MCMCSampler.run for a composition outside the fused kernels' set."""
+    from .rng import PhiloxRNG, resolve_rng
+    from .sampler import _bump, _check_resume
+
+    if keep not in ("samples", "moments", "last"):
+        raise ValueError("keep must be 'samples', 'moments' or 'last'")
+    T = np.float64 if dev.torch_dtype(sampler.dtype) == dev.F64 else np.float32
+    device = sampler.device  # resolved where a device call needs it (draws, a device G)
+    resume = isinstance(u_0, ChainState)
+    if resume:
+        single = False
+        U = np.array(u_0.u, dtype=T)
+    else:
+        if isinstance(u_0, torch.Tensor):
+            u_0 = u_0.detach().cpu().numpy()
+        arr = np.asarray(u_0, dtype=np.float64)
+        single = arr.ndim <= 1
+        U = np.atleast_2d(arr).astype(T).copy()
+        if arr.ndim == 0:
+            U = U.reshape(1, 1)
+    n_chains, k = U.shape
+    n_samples, sample_interval = int(n_samples), int(sample_interval)
+    if n_samples < 0 or sample_interval < 0:
+        raise ValueError("n_samples and sample_interval must be >= 0")
+    if not isinstance(sampler.rng, PhiloxRNG):
+        sampler.rng = resolve_rng(sampler.rng)
+    rng = sampler.rng
+    try:
+        plan = HostPlan(sampler.proposer, sampler.accepter, k)
+    except GenericComposition:
+        plan = None
+    accept_kind = None if plan is None else plan.accept_kind
+    if resume:
+        if accept_kind is not None:
+            _check_resume(u_0, sampler.chain_offset, accept_kind)
+        rng.seed, rng.step = u_0.seed, u_0.step
+        if hasattr(sampler.proposer, "i"):
+            sampler.proposer.i = u_0.proposer_i
+    if isinstance(sampler.accepter, CountedAccepter):
+        sampler.accepter.reset()  # sampler.py:15-16
+    n_burn = max(0, burn_in - sample_interval)  # sampler.py:18
+    # interval 0 records the same state n_samples times (the reference's loop does)
+    eff_interval = sample_interval if sample_interval > 0 else 1
+    rec = _Recorder(keep, n_chains, n_samples, k, single, sample_file)
+    state_dtype = "float64" if T == np.float64 else "float32"
+    prop_i = getattr(sampler.proposer, "i", 0)
+    import time
+
+    t0 = time.perf_counter()
+    calls_np = None
+    # sample_interval 0: burn in, then every sample is the same state (the
+    # reference's loop runs no step between its records, sampler.py:23-28)
+    n_rec = n_samples if sample_interval > 0 else 0
+    if plan is not None:
+        if resume and u_0.dtype == state_dtype and u_0.phi.shape[0] == n_chains:
+            phi = np.array(u_0.phi, dtype=T)
+        else:
+            phi = initial_phi(plan, U, device)
+        acc_np, counts, total = run_structured(plan, U, phi, rng.seed, sampler.chain_offset, rng.step, prop_i,
+                                               n_burn, n_rec, eff_interval, rec, device)
+        ci = 0
+        inner = False
+        for kind, obj in plan.layers:
+            if kind == "count":
+                c = counts[ci]
+                ci += 1
+                _bump(obj, c, acc_np, single)
+                if inner and calls_np is None:
+                    calls_np = c
+            else:
+                inner = True
+    else:
+        phi = np.full(n_chains, np.nan, dtype=T)
+        counted = _counted(sampler.accepter)
+        prev = [(ca.calls, ca.accepts) for ca in counted]
+        counted, per, total = run_generic(sampler.proposer, sampler.accepter, U, rng.seed, sampler.chain_offset,
+                                          rng.step, n_burn, n_rec, eff_interval, rec, device)
+        acc_np = per[id(counted[0])][1] if counted else np.zeros(n_chains, dtype=np.int64)
+        for ca, (c0, a0) in zip(counted, prev):
+            # per-chain arrays for many chains, ints for one (the device path's convention)
+            c, a = per[id(ca)]
+            ca.calls, ca.accepts = c0, a0
+            _bump(ca, c, a, single)
+    if sample_interval == 0:
+        for i in range(n_samples):
+            rec.record(i, U)
+    sampler.last_run_seconds = time.perf_counter() - t0
+    sampler.last_path = "host" if plan is not None else "host-generic"
+    sampler.last_host_reason = reason
+    rng.step += total
+    prop_i += total
+    if hasattr(sampler.proposer, "i"):
+        sampler.proposer.i = prop_i
+    if sampler.verbose and isinstance(sampler.accepter, CountedAccepter):
+        print(f"Acceptance ratio: {sampler.accepter.ratio()}")  # sampler.py:30-31
+    prev_acc = u_0.accepts if resume else 0
+    prev_calls = u_0.calls if (resume and u_0.calls is not None) else 0
+    sampler.state = ChainState(U.copy(), np.asarray(phi).copy(), prev_acc + acc_np,
+                               None if calls_np is None else prev_calls + calls_np, rng.seed, rng.step, prop_i,
+                               state_dtype, chain_offset=sampler.chain_offset, accept_kind=accept_kind)
+    sampler.state.steps_this_run = total
+    if keep == "samples":
+        if rec.sink is not None:
+            return rec.sink.close()
+        return rec.samples[0] if single else rec.samples
+    if keep == "moments":
+        n_post = n_samples * sample_interval
+        if single:
+            return {"sum_u": rec.sum_u[0], "sum_u2": rec.sum_u2[0], "n": n_post}
+        return {"sum_u": rec.sum_u, "sum_u2": rec.sum_u2, "n": n_post}
+    last = U.astype(np.float64)
+    return last[0] if single else last

@@ -83,7 +83,17 @@ class EvolutionPotential(PotentialBase):
 
     # ---------------------------------------------------------- reference form
     def __call__(self, u):
-        """−noise.logpdf(y − G(u)) (potential.py:53-54); u (k,) -> float, (n, k) -> (n,)."""
+        """−noise.logpdf(y − G(u)) (potential.py:53-54); u (k,) -> float, (n, k) -> (n,).
+        A device forward map with diagonal Gaussian noise evaluates on the GPU;
+        a Python G or another noise model evaluates as the reference does."""
+        try:
+            self.device_terms()
+        except UnsupportedOnDevice:
+            single = np.ndim(u) <= 1
+            pts = np.atleast_2d(np.asarray(u, dtype=np.float64))
+            vals = np.array([-self.rho.logpdf(self.y - np.atleast_1d(np.asarray(self.G(p), dtype=np.float64)))
+                             for p in pts], dtype=np.float64).reshape(-1)
+            return float(vals[0]) if single else vals
         single = np.ndim(u) <= 1
         arr = np.asarray(u, dtype=np.float64).reshape(-1, self.G.k)
         t = dev.to_device(arr, dev.F64, dev.resolve_device())

@@ -12,8 +12,11 @@ step (ConstSteppCNProposer / VarSteppCNProposer / ConstStepStandardRWProposer /
 VarStepStandardRWProposer + pCNAccepter or StandardRWAccepter on an
 EvolutionPotential with a device forward map, optionally wrapped in
 CountedAccepter / ConstrainAccepter(BoxConstraint)) runs as one fused HIP
-kernel per block of steps (libipmc ``ipmc_pcn_sweep``).  Any other
-composition raises ``UnsupportedOnDevice``: there is no CPU fallback.
+kernel per block of steps (libipmc ``ipmc_pcn_sweep``).  A composition with
+caller Python code in it -- a Python forward map, a constraint predicate, a
+non-diagonal noise covariance, a user proposer or accepter -- runs the
+host-side step of hostloop.py instead, with the same GPU-drawn Philox stream
+(no composition the kernels can run ever takes that path).
 
 Differences from the reference, all deliberate:
   * randomness is the counter-based Philox stream of rng.py, not PCG64;
@@ -142,6 +145,9 @@ class MCMCSampler:
         # state of the last run (device tensors), for inspection / continuation
         self.state = None
         self.last_run_seconds = None
+        # "device" (fused kernels), "host" / "host-generic" (hostloop.py) for the last run
+        self.last_path = None
+        self.last_run_timing = None
 
     # ------------------------------------------------------------------ run
     def run(self, u_0, n_samples, burn_in=1000, sample_interval=200, keep="samples", sample_file=None,
@@ -158,7 +164,17 @@ class MCMCSampler:
         ``flush_every`` samples) and returns it memory-mapped."""
         if keep not in ("samples", "moments", "last"):
             raise ValueError("keep must be 'samples', 'moments' or 'last'")
-        plan = _Plan(self.proposer, self.accepter)
+        t_entry = time.perf_counter()
+        try:
+            plan = _Plan(self.proposer, self.accepter)
+        except UnsupportedOnDevice as e:
+            # a Python forward map / constraint / noise model or a caller's own
+            # proposer or accepter: the host-side step (hostloop.py), with the
+            # same counter-based draws from the GPU
+            from . import hostloop
+
+            return hostloop.run(self, u_0, n_samples, burn_in, sample_interval, keep, sample_file, str(e))
+        self.last_path = "device"
         device = dev.resolve_device(self.device)
         td = dev.torch_dtype(self.dtype)
         k = plan.G.k
@@ -309,6 +325,8 @@ class MCMCSampler:
             sw.sample_every = 0
 
         t0 = time.perf_counter()
+        ev_first = torch.cuda.Event(enable_timing=True)
+        ev_first.record(torch.cuda.current_stream(device))
         spl = _steps_per_launch(model, n_chains)
         n_burn = max(0, burn_in - sample_interval)  # sampler.py:18
         for c0 in range(0, n_burn, spl):
@@ -383,6 +401,8 @@ class MCMCSampler:
                 samples = writer.flush(i - slot, slot + 1)
         if sink is not None:
             writer.finish()
+        ev_swept = torch.cuda.Event(enable_timing=True)
+        ev_swept.record(torch.cuda.current_stream(device))
         # the host copy of the samples goes to page-locked memory (~57 GB/s
         # instead of ~5 GB/s pageable on the MI355X box, profiles/r1/d2h_probe.txt);
         # allocating it here overlaps the allocation with the queued sweeps
@@ -425,11 +445,18 @@ class MCMCSampler:
             chain_offset=self.chain_offset, accept_kind=accept_kind,
         )
         self.state.steps_this_run = total
+        if keep == "samples" and sink is None and not overlap:
+            host_out.copy_(samples if samples.dtype == torch.float64 else samples.double())
+        # where the wall time went: set-up (H2D, Φ(u0), plan) before the first
+        # launch, the GPU time of all sweeps, and the rest after set-up that the
+        # sweeps do not cover (launch gaps, the copy tail, host epilogue)
+        t_end = time.perf_counter()
+        sweeps_ms = ev_first.elapsed_time(ev_swept)
+        self.last_run_timing = {"total_s": t_end - t_entry, "setup_s": t0 - t_entry, "sweeps_gpu_ms": sweeps_ms,
+                                "tail_ms": (t_end - t0) * 1e3 - sweeps_ms, "copy_overlapped": bool(overlap)}
         if keep == "samples":
             if sink is not None:
                 return sink.close()
-            if not overlap:
-                host_out.copy_(samples if samples.dtype == torch.float64 else samples.double())
             out = host_out.numpy()  # shares the page-locked buffer (kept alive by the array)
             return out[0] if single else out
         if keep == "moments":

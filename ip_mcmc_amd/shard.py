@@ -40,13 +40,18 @@ def gather_chains(local, n_total, group=None):
     return torch.cat(parts, dim=0)
 
 
-def ordered_mean(x):
+def ordered_mean(x, block=1 << 16):
     """Mean over the chain axis (dim 0) in fixed sequential chain order, on the
-    host in float64: identical for every sharding of the same chains."""
+    host in float64: identical for every sharding of the same chains.  The
+    running sum ((0 + row_0) + row_1) + ... is np.cumsum along the chain axis
+    (a strictly sequential accumulate), taken in blocks of rows so that the
+    2^20-chain case needs no full-size temporary."""
     import numpy as np
 
-    a = x.detach().double().cpu().numpy()
+    a = x.detach().double().cpu().numpy() if hasattr(x, "detach") else np.asarray(x, dtype=np.float64)
     acc = np.zeros(a.shape[1:], dtype=np.float64)
-    for row in a:
-        acc = acc + row
+    for i in range(0, a.shape[0], block):
+        blk = a[i : i + block].copy()
+        blk[0] = acc + blk[0]
+        acc = np.cumsum(blk, axis=0)[-1]
     return acc / a.shape[0]

@@ -18,6 +18,26 @@ def test_share_device_needs_gloo():
 def test_help_lists_the_options():
     r = _bench("--help")
     assert r.returncode == 0 and "--scaling" in r.stdout and "--dist-backend" in r.stdout
+    assert "--steps-per-launch" in r.stdout
+
+
+def test_world_size_must_equal_gpus():
+    """Under an external launcher WORLD_SIZE has to match --gpus (refused before any GPU call)."""
+    import os
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4"], cwd=REPO, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
+
+
+def test_auto_steps_per_launch():
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.auto_per_launch(65536) == 1  # the full ensemble fills the GPU: one step per launch
+    assert bench.auto_per_launch(8192) == 8  # strong scaling over 8 GPUs: room to speculate
+    assert bench.auto_per_launch(1) == 64
 
 
 def _committed_lines():

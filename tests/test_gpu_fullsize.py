@@ -1,4 +1,4 @@
-"""Parity at BASELINE's full sizes (configs 4 and 5), through the C-ABI / torch ops.
+"""Parity at BASELINE's full sizes (configs 2, 4 and 5), through the C-ABI / torch ops.
 
 The oracle cannot re-run whole ensembles of this size in seconds, so each test
 runs the full ensemble on the device once and checks (a) sampled chains
@@ -56,12 +56,12 @@ def test_cfg5_gpu_share_full_length(dev, orc, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_cfg4_full_ensemble_and_shards(dev, orc, dtype):
-    """Config 4: Burgers N=256, fixed dt 1e-3 x 1000, beta 0.15, all 16 384 chains
-    in one launch == the eight 2 048-chain shards of an 8-GPU run; sampled chains
-    == the oracle."""
+    """Config 4: viscous Burgers (nu = 1e-3) N=256, fixed dt 1e-3 x 1000, beta
+    0.15, all 16 384 chains in one launch == the eight 2 048-chain shards of an
+    8-GPU run; sampled chains == the oracle."""
     from ip_mcmc_amd import BurgersOperator
 
-    op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000)
+    op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000, nu=1e-3)
     C_, P = 16384, 8
     rng = np.random.default_rng(44)
     U0 = (0.25 * rng.normal(size=(C_, 3))).astype(_np(dtype)).astype(np.float64)
@@ -117,3 +117,42 @@ def test_headline_samples_overlapped_copy(dev, dtype, monkeypatch):
     assert a.shape == (C_, 20, d) and a.dtype == np.float64
     assert np.array_equal(a, b)
     assert np.array_equal(a[:, -1, :], np.asarray(ua, dtype=np.float64))
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_cfg2_full_shape(dev, orc, dtype):
+    """Config 2 as SURVEY §8(d) defines it (tools/config_bench.cfg2_problem):
+    Lorenz-63, 500 RK4 steps of 0.01 from the spun-up state, prior
+    N(0, diag(1, 1, 0.1)), y = the truth's long-run moment means, Γ = 0.5²·diag(var
+    of the moments), beta 0.2, 4 096 chains.  One launch of 128 pCN steps with
+    the automatic plan -- ipmc_plan_sweep reports the speculative sweep of
+    width 16 -- and every chain's state, Φ, accept and call counts equal the
+    oracle's sequential chain."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import ctypes as C
+
+    import config_bench as CB
+    from ip_mcmc_amd import _abi
+    from ip_mcmc_amd._lib import call
+
+    op, y, ginv, sq, beta = CB.cfg2_problem()
+    C_, n = 4096, 128
+    rng = np.random.default_rng(22)
+    U0 = (sq * rng.normal(size=(C_, 3))).astype(_np(dtype)).astype(np.float64)  # prior draws
+    phi0 = _device_phi(op, U0, y, ginv, dtype, dev).astype(np.float64)
+    assert np.array_equal(phi0, orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64))
+    m, _ = op.model(dtype, dev)
+    sw = _abi.IpmcSweep()
+    sw.dtype, sw.n_chains, sw.n_steps, sw.spec_width = (_abi.F64 if dtype == torch.float64 else _abi.F32), C_, n, 0
+    plan = _abi.IpmcPlan()
+    call("ipmc_plan_sweep", C.byref(m), C.byref(sw), C.byref(plan))
+    assert plan.spec_width == 16
+    d = _sweep_device(op, U0, phi0, y, ginv, sq, beta, 2, 0, n, dtype, dev, spec=0)
+    o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, beta, 2, 0, n, dtype)
+    for key in ("u", "phi", "acc", "calls"):
+        assert np.array_equal(d[key], o[key]), key
+    rate = o["acc"].sum() / (C_ * n)
+    assert 0.01 < rate < 0.99, rate

@@ -379,14 +379,16 @@ def test_sampler_l96_chain_matches_reference_fixture(dev, golden):
     assert np.array_equal(out, golden["l96c_samples"])
 
 
-def test_sampler_rejects_host_callables(dev):
+def test_sampler_runs_host_callables_on_the_host_path(dev):
+    """A Python G is no longer refused: it takes the host-side step
+    (hostloop.py) with the GPU's draws."""
     from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, MCMCSampler,
-                             UnsupportedOnDevice, pCNAccepter)
+                             pCNAccepter)
 
     pot = EvolutionPotential(lambda u: u, np.zeros(2), GaussianDistribution(np.zeros(2), np.eye(2)))
     s = MCMCSampler(ConstSteppCNProposer(0.5, GaussianDistribution(np.zeros(2), np.eye(2))), pCNAccepter(pot), 1)
-    with pytest.raises(UnsupportedOnDevice):
-        s.run(np.zeros(2), 2, 0, 1)
+    out = s.run(np.zeros(2), 2, 0, 1)
+    assert out.shape == (2, 2) and s.last_path == "host"
 
 
 # ---------------------------------------------------------------- Burgers

@@ -1,0 +1,256 @@
+"""The host-side step (ip_mcmc_amd/hostloop.py) on the reference's own fixtures.
+
+On this CPU-only machine the draws come from the oracle's Philox restatement
+(bit-identical to ipmc_pcn_draws, which tests/test_gpu_hostloop.py checks on
+the GPU); everything else is the product code: the composition parsing, the
+proposal arithmetic, Python forward maps and predicates, the accept rule and
+the counters.  The fixtures are the reference sampler's chains with the same
+draws injected (tests/golden/make_golden.py): config 1's closure
+G(u) = np.dot(g, u) (stuart_examples.py:69-70), a constraint predicate
+(accepter.py:39-55), a non-diagonal prior, and the reference Burgers study's
+own is_valid_IC + VarStepStandardRWProposer(PWLinear) + StandardRWAccepter.
+"""
+import numpy as np
+import pytest
+
+from ip_mcmc_amd import (ConstrainAccepter, ConstSteppCNProposer, CountedAccepter, EvolutionPotential,
+                         GaussianDistribution, MCMCSampler, PhiloxRNG, ProbabilisticAccepter, ProposerBase,
+                         StandardRWAccepter, VarStepStandardRWProposer, PWLinear, pCNAccepter, pCNProposer)
+from ip_mcmc_amd import hostloop
+
+
+def _oracle_w(orc):
+    def draws(seed, off, C_, step0, n, k, T, sq, chol, device=None):
+        w = np.empty((n, C_, k), dtype=T)
+        lr = np.empty((n, C_))
+        for s in range(n):
+            xi = orc.normals(seed, off, C_, step0 + s, k).astype(T)
+            if chol is None:
+                w[s] = np.asarray(sq, dtype=np.float64).astype(T)[None, :] * xi
+            else:
+                L = np.asarray(chol, dtype=np.float64).astype(T)
+                acc = np.zeros((C_, k), dtype=T)
+                for j in range(k):
+                    a = np.zeros(C_, dtype=T)
+                    for i in range(j + 1):
+                        a = a + xi[:, i] * L[j, i]
+                    acc[:, j] = a
+                w[s] = acc
+            lr[s] = orc.det_log(orc.uniforms(seed, off, C_, step0 + s))
+        return w, lr
+
+    return draws
+
+
+def _oracle_raw(orc):
+    def draws(seed, off, C_, step0, n, k, device=None):
+        xi = np.stack([orc.normals(seed, off, C_, step0 + s, k) for s in range(n)])
+        r = np.stack([orc.uniforms(seed, off, C_, step0 + s) for s in range(n)])
+        return xi, r
+
+    return draws
+
+
+@pytest.fixture
+def odraws(orc, monkeypatch):
+    monkeypatch.setitem(hostloop.DRAWS, "w", _oracle_w(orc))
+    monkeypatch.setitem(hostloop.DRAWS, "raw", _oracle_raw(orc))
+
+
+def _lin(golden):
+    gamma, beta, seed, n_samples, burn_in, interval = golden["lin_meta"]
+    g = golden["lin_g"]
+
+    def G(u):  # stuart_examples.py:69-70, the reference's closure
+        return np.dot(g, u)
+
+    return G, gamma, beta, int(seed), int(n_samples), int(burn_in), int(interval)
+
+
+def test_python_G_single_chains_match_reference_fixture(odraws, golden):
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    for chain in range(4):
+        acc = CountedAccepter(pCNAccepter(pot))
+        s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))), acc,
+                        PhiloxRNG(seed), chain_offset=chain)
+        out = s.run(np.zeros(4), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+        assert s.last_path == "host"
+        assert out.shape == (n_samples, 4)
+        np.testing.assert_array_equal(out, golden["lin_samples"][chain])
+        assert acc.accepts == int(golden["lin_counts"][chain, 1])
+        assert acc.calls == int(golden["lin_counts"][chain, 0])
+
+
+def test_python_G_many_chains_match_reference_fixture(odraws, golden):
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    acc = CountedAccepter(pCNAccepter(pot))
+    s = MCMCSampler(pCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))), acc, PhiloxRNG(seed))
+    out = s.run(np.zeros((4, 4)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    np.testing.assert_array_equal(out, golden["lin_samples"])
+    assert np.array_equal(acc.accepts, golden["lin_counts"][:, 1])
+    assert np.array_equal(acc.calls, golden["lin_counts"][:, 0])
+    # the Philox position carries over like one Generator (code.org:12-13)
+    assert s.rng.step == max(0, burn_in - interval) + n_samples * interval
+
+
+def test_user_proposer_and_accepter_match_reference_fixture(odraws, golden):
+    """The generic tier: a caller's own ProposerBase / ProbabilisticAccepter
+    subclasses (the reference's classes, restated) get the same draws through
+    rng.multivariate_normal / rng.random."""
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+
+    class MyPCN(ProposerBase):  # proposer.py:59-82
+        def __init__(self, beta, prior):
+            self.beta, self.prior = beta, prior
+
+        def __call__(self, u, rng):
+            w = rng.multivariate_normal(mean=np.zeros(4), cov=self.prior.covariance)
+            return np.sqrt(1 - self.beta**2) * u + self.beta * w
+
+    noise = GaussianDistribution(0, gamma**2)
+
+    class MyAccepter(ProbabilisticAccepter):  # accepter.py:109-122
+        def accept_probability(self, u, v):
+            phi = lambda x: -noise.logpdf(golden["lin_y"] - G(x))
+            return np.exp(phi(u) - phi(v))
+
+    acc = CountedAccepter(MyAccepter())
+    s = MCMCSampler(MyPCN(beta, GaussianDistribution(np.zeros(4), np.eye(4))), acc, PhiloxRNG(seed))
+    out = s.run(np.zeros((4, 4)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    assert s.last_path == "host-generic"
+    np.testing.assert_array_equal(out, golden["lin_samples"])
+    assert np.array_equal(acc.accepts, golden["lin_counts"][:, 1])
+
+
+def test_constraint_predicate_matches_reference_fixture(odraws, golden):
+    gamma, beta, seed, n_samples, burn_in, interval = golden["con_meta"]
+    g, lo, hi = golden["con_g"], golden["con_lo"], golden["con_hi"]
+    pot = EvolutionPotential(lambda u: np.dot(g, u), golden["con_y"], GaussianDistribution(0, gamma**2))
+    inner = CountedAccepter(pCNAccepter(pot))
+    acc = ConstrainAccepter(inner, lambda v: bool(np.all(lo < v) and np.all(v < hi)))
+    s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))), acc,
+                    PhiloxRNG(int(seed)))
+    out = s.run(np.zeros((3, 4)), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+    np.testing.assert_array_equal(out, golden["con_samples"])
+    assert np.array_equal(inner.calls, golden["con_counts"][:, 0])
+    assert np.array_equal(inner.accepts, golden["con_counts"][:, 1])
+    assert np.array_equal(s.state.calls, golden["con_counts"][:, 0])
+
+
+def test_dense_prior_with_python_G_matches_reference_fixture(odraws, golden):
+    gamma, beta, seed, n_samples, burn_in, interval = golden["dpl_meta"]
+    g = golden["dpl_g"]
+    k = g.shape[-1]
+    pot = EvolutionPotential(lambda u: np.atleast_1d(np.dot(g, u)), golden["dpl_y"],
+                             GaussianDistribution(np.zeros(len(golden["dpl_y"])),
+                                                  gamma**2 * np.eye(len(golden["dpl_y"]))))
+    s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(k), golden["dpl_cov"])),
+                    CountedAccepter(pCNAccepter(pot)), PhiloxRNG(int(seed)))
+    out = s.run(np.zeros((3, k)), n_samples=int(n_samples), burn_in=int(burn_in), sample_interval=int(interval))
+    np.testing.assert_array_equal(out, golden["dpl_samples"])
+    assert np.array_equal(s.accepter.accepts, golden["dpl_accepts"])
+
+
+def test_burgers_study_rw_with_is_valid_IC_matches_reference_fixture(orc, odraws, golden):
+    """burgers_beta.py's RW study: VarStepStandardRWProposer(PWLinear) +
+    StandardRWAccepter inside ConstrainAccepter(is_valid_IC) -- the predicate a
+    Python function as the reference writes it (burgers_wasserstein_chain.py:47-55),
+    G a Python function (here the oracle's CFL Rusanov + Measurer; on the GPU
+    the device operator)."""
+    from ip_mcmc_amd import BurgersOperator
+
+    meta = golden["bch_meta"]
+    N, gamma, sigma_p, beta, seed = int(meta[0]), meta[1], meta[2], meta[3], int(meta[4])
+    n_samples, burn_in, interval = int(meta[5]), int(meta[6]), int(meta[7])
+    d_s, d_e, l = meta[8], meta[9], meta[10]
+    pm = golden["bch_prior_mean"]
+    op = BurgersOperator(prior_mean=pm, N=N, T=1.0, dt_mode="cfl", arith="reference")
+
+    def G(u):
+        return orc.forward(op, np.asarray(u)[None, :])[0]
+
+    def is_valid_IC(u):  # burgers_wasserstein_chain.py:47-55, on the perturbation's prior-mean shift
+        return -1 < (pm + u)[2] < 1
+
+    prior = GaussianDistribution(np.zeros(3), sigma_p**2 * np.eye(3))
+    pot = EvolutionPotential(G, golden["bch_y"], GaussianDistribution(np.zeros(5), gamma**2 * np.eye(5)))
+    inner = CountedAccepter(StandardRWAccepter(pot, prior))
+    acc = ConstrainAccepter(inner, is_valid_IC)
+    s = MCMCSampler(VarStepStandardRWProposer(PWLinear(d_s, d_e, l), prior), acc, PhiloxRNG(seed + 1))
+    out = s.run(np.zeros((3, 3)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    np.testing.assert_array_equal(out, golden["bch_rw_samples"])
+    assert np.array_equal(inner.calls, golden["bch_rw_counts"][:, 0])
+    assert np.array_equal(inner.accepts, golden["bch_rw_counts"][:, 1])
+
+
+def test_dense_noise_follows_the_reference_accept_rule(odraws, orc):
+    """A non-diagonal noise covariance (no device form): the host loop's chains
+    equal a direct restatement of the reference step (sampler.py:35-41 with
+    pCNAccepter on -noise.logpdf, accepter.py:62) under the same draws."""
+    rng = np.random.default_rng(3)
+    A = rng.normal(size=(3, 2))
+    Gam = np.array([[0.3, 0.1, 0.0], [0.1, 0.2, 0.05], [0.0, 0.05, 0.25]])
+    noise = GaussianDistribution(np.zeros(3), Gam)
+    y = A @ np.array([0.5, -1.0]) + rng.multivariate_normal(np.zeros(3), Gam)
+    G = lambda u: A @ u
+    beta, seed, C_, n = 0.4, 77, 5, 60
+    s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(2), np.eye(2))),
+                    CountedAccepter(pCNAccepter(EvolutionPotential(G, y, noise))), PhiloxRNG(seed))
+    out = s.run(np.zeros((C_, 2)), n_samples=n, burn_in=1, sample_interval=1)
+    # the reference step, one chain at a time
+    ref = np.zeros((C_, n, 2))
+    for c in range(C_):
+        u = np.zeros(2)
+        for t in range(n):
+            xi = orc.normals(seed, c, 1, t, 2)[0]
+            v = np.sqrt(1 - beta**2) * u + beta * xi
+            r = orc.uniforms(seed, c, 1, t)[0]
+            phi = lambda x: -noise.logpdf(y - G(x))
+            if np.exp(phi(u) - phi(v)) > r:
+                u = v
+            ref[c, t] = u
+    np.testing.assert_array_equal(out, ref)
+    assert 0 < np.sum(s.accepter.accepts) < C_ * n
+
+
+def test_moments_last_and_interval_zero(odraws, golden):
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    prior = GaussianDistribution(np.zeros(4), np.eye(4))
+    s = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed))
+    smp = s.run(np.zeros((4, 4)), n_samples=6, burn_in=3, sample_interval=1)
+    s2 = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed))
+    mom = s2.run(np.zeros((4, 4)), n_samples=6, burn_in=3, sample_interval=1, keep="moments")
+    np.testing.assert_array_equal(mom["sum_u"], smp.sum(axis=1))
+    assert mom["n"] == 6
+    s3 = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed))
+    last = s3.run(np.zeros((4, 4)), n_samples=6, burn_in=3, sample_interval=1, keep="last")
+    np.testing.assert_array_equal(last, smp[:, -1])
+    s4 = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed))
+    z = s4.run(np.zeros(4), n_samples=3, burn_in=5, sample_interval=0)
+    assert z.shape == (3, 4) and np.array_equal(z[0], z[2]) and s4.rng.step == 5
+
+
+def test_resume_continues_exactly(odraws, golden):
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    prior = GaussianDistribution(np.zeros(4), np.eye(4))
+    full = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed)).run(
+        np.zeros((4, 4)), n_samples=10, burn_in=1, sample_interval=3)
+    s = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed))
+    a = s.run(np.zeros((4, 4)), n_samples=4, burn_in=1, sample_interval=3)
+    st = s.checkpoint()
+    s2 = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(0))
+    b = s2.run(st, n_samples=6, burn_in=0, sample_interval=3)
+    np.testing.assert_array_equal(np.concatenate([a, b], axis=1), full)
+
+
+def test_python_potential_value_is_the_reference_formula(golden):
+    """EvolutionPotential.__call__ with a Python G: −noise.logpdf(y − G(u))
+    (potential.py:53-54) = the reference's values in the fixture."""
+    G, gamma, *_ = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    vals = np.array([pot(u) for u in golden["lin_phi_u"]])
+    np.testing.assert_allclose(vals, golden["lin_phi"], rtol=1e-14, atol=1e-13)

@@ -2,7 +2,9 @@
 
   python tools/config_bench.py [cfg2 cfg4 cfg4full cfg5 ...]
 
-cfg2     Lorenz-63, 500 RK4 steps, 4 096 chains
+cfg2     Lorenz-63, 500 RK4 steps, 4 096 chains; SURVEY §8(d): prior N(0, diag(1, 1, 0.1)),
+         y = the long-run moment means of the truth, Γ = r²·diag(var of the instantaneous moments),
+         r = 0.5 (lorenz_mcmc.py:106-112's construction)
 cfg4     Burgers N=256, fixed dt 1e-3 x 1000, 2 048 chains (= 16 384 / 8 GPUs)
 cfg4full Burgers as cfg4 with all 16 384 chains on one GPU
 cfg4cfl  Burgers N=256, reference CFL time stepping, 2 048 chains
@@ -28,8 +30,42 @@ from ip_mcmc_amd import (BurgersOperator, Lorenz63Operator, Lorenz96Operator, Tw
 from ip_mcmc_amd._lib import call, lib  # noqa: E402
 
 
+def l63_truth_moments(theta=(10.0, 28.0, 8.0 / 3.0), dt=0.01, spinup=1000, n=50000):
+    """Mean and variance over a long truth trajectory (T = n·dt after the
+    spin-up) of the instantaneous moments (x, y, z, x², y², z²): the data and
+    the noise scale of config 2, built as lorenz_mcmc.py:100-112 builds its own
+    (moment_function over a long simulation, np.mean / np.var along time)."""
+    s, r, b = theta
+    x = Lorenz63Operator.spinup(theta, dt=dt, n_steps=spinup)
+    f = lambda x: np.array([s * (x[1] - x[0]), x[0] * (r - x[2]) - x[1], x[0] * x[1] - b * x[2]])
+    traj = np.empty((n, 3))
+    for t in range(n):
+        k1 = f(x)
+        k2 = f(x + 0.5 * dt * k1)
+        k3 = f(x + 0.5 * dt * k2)
+        k4 = f(x + dt * k3)
+        x = x + dt / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
+        traj[t] = x
+    mom = np.concatenate([traj, traj**2], axis=1)
+    return mom.mean(axis=0), mom.var(axis=0)
+
+
+CFG2_R = 0.5  # noise level r (lorenz_mcmc.py:92)
+
+
+def cfg2_problem():
+    """(operator, y, 1/γ, prior sqrt-diagonal, beta) of config 2."""
+    x0 = Lorenz63Operator.spinup(n_steps=1000)
+    op = Lorenz63Operator(x0=x0, dt=0.01, n_steps=500)
+    mean, var = l63_truth_moments()
+    return op, mean, 1.0 / (CFG2_R * np.sqrt(var)), np.array([1.0, 1.0, np.sqrt(0.1)]), 0.2
+
+
 def make(cfg):
     if cfg == "cfg2":
+        op, y, ginv, sq, beta = cfg2_problem()
+        return op, 4096, beta, sq, 80 * 500, (y, ginv)
+    if cfg == "cfg2g1":  # round 1-2's config 2 (gamma = 1 for every moment, y = G(0) + N(0, 1))
         x0 = Lorenz63Operator.spinup(n_steps=1000)
         op = Lorenz63Operator(x0=x0, dt=0.01, n_steps=500)
         return op, 4096, 0.2, np.array([1.0, 1.0, np.sqrt(0.1)]), 80 * 500, 1.0
@@ -64,9 +100,13 @@ def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
     m, _ = op.model(dtype, dev)
     u = torch.zeros((n, op.k), dtype=dtype, device=dev)
-    g0 = op.forward_device(u[:1].clone())[0].double().cpu().numpy()
-    y = t(np.nan_to_num(g0) + gamma * np.random.default_rng(1).normal(size=op.q))
-    gi, sqt = t(np.full(op.q, 1 / gamma)), t(sq)
+    if isinstance(gamma, tuple):  # (y, 1/γ) given by the config
+        y, gi = t(gamma[0]), t(gamma[1])
+    else:
+        g0 = op.forward_device(u[:1].clone())[0].double().cpu().numpy()
+        y = t(np.nan_to_num(g0) + gamma * np.random.default_rng(1).normal(size=op.q))
+        gi = t(np.full(op.q, 1 / gamma))
+    sqt = t(sq)
     phi = torch.empty(n, dtype=dtype, device=dev)
     adt = _abi.F64 if dtype == torch.float64 else _abi.F32
     st = torch.cuda.current_stream(dev).cuda_stream

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 3 GPU session (tools/gpu_session.sh stops at the first fault/abort/time-out).
+#   tools/sessions/r3.sh <name>   -- the steps of session <name>
+cd "$GRAFT_REPO_ROOT" || exit 2
+export TMPDIR=/tmp
+PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread -rf"
+case "$1" in
+  a)  # host loop, FMA-vs-reference, full-size configs, bench plumbing; then everything
+    tools/gpu_session.sh \
+      "new_tests:600:$PYT -v -s tests/test_gpu_hostloop.py tests/test_gpu_arith_agreement.py tests/test_gpu_fullsize.py tests/test_gpu_bench_dist.py -m gpu" \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" \
+      "bench:400:python bench.py > gpurun_out/bench_line.json" \
+      "arith:400:python tools/arith_agreement.py 100 0.2 0.05 0.02 > gpurun_out/arith_agreement.jsonl" \
+      "cfg2:300:python tools/config_bench.py cfg2@128 cfg2g1@128 cfg2 > gpurun_out/cfg2.jsonl" \
+      "stuart:400:python examples/stuart_reference.py > gpurun_out/stuart_reference.jsonl"
+    ;;
+  *) echo "unknown session $1"; exit 2 ;;
+esac
