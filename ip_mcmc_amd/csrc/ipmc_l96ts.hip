@@ -1,12 +1,16 @@
 // Two-scale Lorenz-96 (lorenz.py:44-101 with J > 0) forward map, observed by
 // the time-averaged moment function of lorenz_mcmc.py:17-40, and its pCN sweep.
 //
-// Layout: one chain per group of K consecutive lanes, floor(64/K) chains per
-// wave (groups need not be power-of-two aligned: K=6 packs 10 chains = 60
-// live lanes per wave); lane k owns the slow variable X_k and its fast block
-// Y_{k,0..J-1} in VGPRs (1+J values per RK4 array).  The fast blocks are cyclic inside the
-// block (np.roll of Y_in[k, :]) so they never leave the lane; the slow
-// neighbours X_{k-2}, X_{k-1}, X_{k+1} (cyclic mod K) come by ds_bpermute.
+// Layout: one chain per group of L = K/SPL consecutive lanes, floor(64/L)
+// chains per wave (groups need not be power-of-two aligned: K=6 at SPL 1 packs
+// 10 chains = 60 live lanes per wave); lane i owns the SPL slow variables
+// X_{i*SPL..i*SPL+SPL-1} and their fast blocks Y_{k,0..J-1} in VGPRs (1+J
+// values per slow variable and RK4 array).  The fast blocks are cyclic inside
+// the block (np.roll of Y_in[k, :]) so they never leave the lane; the slow
+// neighbours X_{k-2}, X_{k-1}, X_{k+1} (cyclic mod K) of the lane's first and
+// last slow variables come from the neighbouring lanes: by ds_bpermute in
+// general, by one DPP quad_perm swap when L = 2 (SPL 3 for K = 6), and not at
+// all when L = 1 (SPL 6 for K = 6: the whole chain in one lane).
 // theta = (F, h, b) = theta0 + u is the same on every lane of the group.
 // Lane k accumulates the five moments of slot k; Φ sums the 5K residuals in
 // observation order (every lane gathers them, so all lanes hold Φ).
@@ -21,6 +25,13 @@ constexpr int kTsBlock = 256;
 #define IPMC_TS_PK 1
 #endif
 
+// SPL 3 and 6 are compiled for K = 6 (the reference's K=6 J=4 study,
+// lorenz_mcmc.py:87-88): lanes per chain fixed at 2 (DPP halos) and 1 (none).
+template <int SPL>
+constexpr int ts_fixed_lanes() {
+  return SPL == 3 ? 2 : (SPL == 6 ? 1 : 0);
+}
+
 // Occupancy target (waves per SIMD) for the sweep kernel: 4 RK4 arrays of
 // 1 + J values per lane plus the chain state.
 template <typename T, int J, int SPL>
@@ -28,6 +39,8 @@ constexpr int ts_waves() {
 #ifdef IPMC_TS_WAVES  // layout experiments (tools/)
   return IPMC_TS_WAVES;
 #endif
+  if constexpr (SPL == 6) return sizeof(T) == 8 ? 1 : 2;
+  if constexpr (SPL == 3) return sizeof(T) == 8 ? 2 : 3;
   if constexpr (SPL == 2) return sizeof(T) == 8 ? (J <= 4 ? 3 : 2) : (J <= 2 ? 4 : (J <= 8 ? 3 : 2));
   return sizeof(T) == 8 ? (J <= 4 ? 4 : (J <= 10 ? 3 : 2)) : (J <= 2 ? 5 : (J <= 8 ? 4 : (J <= 10 ? 3 : 2)));
 }
@@ -147,6 +160,29 @@ __device__ __forceinline__ T block_sum(const T (&s)[1 + J]) {
   return np_pairwise<T, J>(y, 0);
 }
 
+// Slow neighbours of a lane holding SPL >= 2 slow variables Xo: p1 = X_{k0-1},
+// p2 = X_{k0-2} (the previous lane's last two) and n0 = X_{k0+SPL} (the next
+// lane's first), cyclic over the group's L = K/SPL lanes.
+template <int SPL, typename T>
+__device__ __forceinline__ void ts_halo(const T (&Xo)[SPL], const TsCtx& c, T& p1, T& p2, T& n0) {
+  constexpr int LF = ts_fixed_lanes<SPL>();
+  if constexpr (LF == 1) {  // the whole ring in this lane
+    p1 = Xo[SPL - 1];
+    p2 = Xo[SPL - 2];
+    n0 = Xo[0];
+  } else if constexpr (LF == 2) {  // previous = next = the other lane of the (pair-aligned) group
+    p1 = dpp<qperm(1, 0, 3, 2)>(Xo[SPL - 1]);
+    p2 = dpp<qperm(1, 0, 3, 2)>(Xo[SPL - 2]);
+    n0 = dpp<qperm(1, 0, 3, 2)>(Xo[0]);
+  } else {
+    const int L = c.K / SPL;
+    const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
+    p1 = shfl(Xo[SPL - 1], prev);
+    p2 = shfl(Xo[SPL - 2], prev);
+    n0 = shfl(Xo[0], next);
+  }
+}
+
 // One classical RK4 stage over the lane's SPL slow variables k = sub*SPL + a
 // and their fast blocks, with each rate k consumed as soon as it is computed:
 //   STAGE 1: acc = k;           out = base + c*k     (in = x, out = xs)
@@ -181,10 +217,8 @@ __device__ __forceinline__ void ts_stage(T (&in)[SPL][1 + J], T (&out)[SPL][1 + 
     const T xp1 = __shfl(Xo[0], c.base + (c.sub + 1) % L, 64);
     kX[0] = ts_slow<T, FM>(Xo[0], xm1, xm2, xp1, kc, yb[0]);
   } else {
-    const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
-    const T p1 = __shfl(Xo[SPL - 1], prev, 64);  // X_{k0-1}
-    const T p2 = __shfl(Xo[SPL - 2], prev, 64);  // X_{k0-2}
-    const T n0 = __shfl(Xo[0], next, 64);        // X_{k0+SPL}
+    T p1, p2, n0;  // X_{k0-1}, X_{k0-2}, X_{k0+SPL}
+    ts_halo<SPL, T>(Xo, c, p1, p2, n0);
 #pragma unroll
     for (int a = 0; a < SPL; ++a) {
       const T xm1 = a >= 1 ? Xo[a - 1] : p1;
@@ -268,10 +302,8 @@ __device__ __forceinline__ void ts_stage_pk(float (&xin)[SPL], f32x2 (&yin)[SPL]
     const float xp1 = __shfl(Xo[0], c.base + (c.sub + 1) % L, 64);
     kX[0] = ts_slow<float, FM>(Xo[0], xm1, xm2, xp1, kc, ybk[0]);
   } else {
-    const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
-    const float p1 = __shfl(Xo[SPL - 1], prev, 64);
-    const float p2 = __shfl(Xo[SPL - 2], prev, 64);
-    const float n0 = __shfl(Xo[0], next, 64);
+    float p1, p2, n0;
+    ts_halo<SPL, float>(Xo, c, p1, p2, n0);
 #pragma unroll
     for (int a = 0; a < SPL; ++a) {
       const float xm1 = a >= 1 ? Xo[a - 1] : p1;
@@ -367,11 +399,12 @@ __device__ float ts_phi_pk(const ipmc_model& m, const float (&v)[3], const TsCtx
   if (y) {
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
-      for (int kk = 0; kk < K; ++kk) {  // observation order: slow variable kk of moment b
-        float mine = r[0][b];
-        if constexpr (SPL == 2) mine = (kk & 1) ? r[1][b] : r[0][b];
-        const float val = __shfl(mine, c.base + kk / SPL, 64);
-        s = madd<FM>(val, val, s);
+      for (int l = 0; l < K / SPL; ++l) {  // observation order: slow variable l*SPL + a of moment b
+#pragma unroll
+        for (int a = 0; a < SPL; ++a) {
+          const float val = __shfl(r[a][b], c.base + l, 64);
+          s = madd<FM>(val, val, s);
+        }
       }
     }
   }
@@ -439,11 +472,12 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
   if (y) {
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
-      for (int kk = 0; kk < K; ++kk) {  // observation order: slow variable kk of moment b
-        T mine = r[0][b];
-        if constexpr (SPL == 2) mine = (kk & 1) ? r[1][b] : r[0][b];
-        const T val = __shfl(mine, c.base + kk / SPL, 64);
-        s = madd<FM>(val, val, s);
+      for (int l = 0; l < K / SPL; ++l) {  // observation order: slow variable l*SPL + a of moment b
+#pragma unroll
+        for (int a = 0; a < SPL; ++a) {
+          const T val = __shfl(r[a][b], c.base + l, 64);
+          s = madd<FM>(val, val, s);
+        }
       }
     }
   }
@@ -588,16 +622,26 @@ static int64_t ts_blocks(int G, int64_t n) {
 
 // Slow variables per lane: 2 when K is even, a chain would otherwise fill a
 // wave alone (K > 32: K=36 packs 3 chains = 54 lanes instead of 1 = 36) and the
-// doubled state still fits (J <= 10); 1 otherwise.  lanes_per_chain = K/2 or K
-// selects it explicitly.  -1: unsupported request.
+// doubled state still fits (J <= 10); for K = 6 with J <= 4 (the thesis
+// problem) kTs6Spl: 3 = pairs of lanes, all 64 lanes live, halos by one DPP
+// swap (6 lanes per chain leave 4 idle lanes per wave and ds_bpermute halos);
+// 1 otherwise.  lanes_per_chain = K, K/2 (K even, J <= 10) or, for K = 6 and
+// J <= 4, 2 or 1 selects it explicitly.  -1: unsupported request.
+#ifndef IPMC_TS6_SPL  // layout experiments (tools/)
+#define IPMC_TS6_SPL 3
+#endif
 static int ts_spl(const ipmc_model& m, const ipmc_sweep* s) {
   const int K = m.dim, J = m.fast_per_slow;
   const bool two_ok = (K % 2 == 0) && J <= 10;
+  const bool six_ok = (K == 6) && J <= 4;
   if (s && s->lanes_per_chain > 0) {
     if (s->lanes_per_chain == K) return 1;
     if (two_ok && s->lanes_per_chain == K / 2) return 2;
+    if (six_ok && s->lanes_per_chain == 2) return 3;
+    if (six_ok && s->lanes_per_chain == 1) return 6;
     return -1;
   }
+  if (six_ok) return IPMC_TS6_SPL;
   return (two_ok && K > 32) ? 2 : 1;
 }
 
@@ -623,7 +667,7 @@ static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) 
   switch (m.fast_per_slow) {
 #define IPMC_J(J)                                                                                                  \
   case J:                                                                                                          \
-    if constexpr (SPL == 1 || J <= 10) {                                                                           \
+    if constexpr (SPL == 1 || (SPL == 2 && J <= 10) || (SPL > 2 && J <= 4)) {                                     \
       hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM, SPL>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, \
                          S);                                                                                       \
       return check_launch("l96ts_sweep_kernel");                                                                   \
@@ -643,7 +687,7 @@ static int ts_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* 
   switch (m.fast_per_slow) {
 #define IPMC_J(J)                                                                                                 \
   case J:                                                                                                         \
-    if constexpr (SPL == 1 || J <= 10) {                                                                          \
+    if constexpr (SPL == 1 || (SPL == 2 && J <= 10) || (SPL > 2 && J <= 4)) {                                    \
       if (phi)                                                                                                    \
         hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, SPL, true>), dim3((unsigned)blocks), dim3(kTsBlock), 0,   \
                            st, m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                          \
@@ -667,14 +711,19 @@ int l96ts_sweep(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) {
   }
   const int spl = ts_spl(m, &s);
   if (spl < 0) {
-    set_error("two-scale Lorenz-96: lanes_per_chain must be K or (K even, J <= 10) K/2");
+    set_error("two-scale Lorenz-96: lanes_per_chain must be K, (K even, J <= 10) K/2 or (K = 6, J <= 4) 2 or 1");
     return IPMC_ERR_UNSUPPORTED;
   }
   const bool fm = m.arith == IPMC_ARITH_FMA;
-  if (spl == 2) {
-    if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true, 2>(m, s, st) : ts_sweep_t<double, false, 2>(m, s, st);
-    return fm ? ts_sweep_t<float, true, 2>(m, s, st) : ts_sweep_t<float, false, 2>(m, s, st);
+#define IPMC_TS_SPL_SWEEP(P)                                                                                       \
+  if (spl == P) {                                                                                                  \
+    if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true, P>(m, s, st) : ts_sweep_t<double, false, P>(m, s, st); \
+    return fm ? ts_sweep_t<float, true, P>(m, s, st) : ts_sweep_t<float, false, P>(m, s, st);                       \
   }
+  IPMC_TS_SPL_SWEEP(2)
+  IPMC_TS_SPL_SWEEP(3)
+  IPMC_TS_SPL_SWEEP(6)
+#undef IPMC_TS_SPL_SWEEP
   if (s.dtype == IPMC_F64) return fm ? ts_sweep_t<double, true, 1>(m, s, st) : ts_sweep_t<double, false, 1>(m, s, st);
   return fm ? ts_sweep_t<float, true, 1>(m, s, st) : ts_sweep_t<float, false, 1>(m, s, st);
 }
@@ -686,7 +735,7 @@ int l96ts_plan(const ipmc_model& m, const ipmc_sweep& s, int& lanes, int& spec) 
   }
   const int spl = ts_spl(m, &s);
   if (spl < 0) {
-    set_error("two-scale Lorenz-96: lanes_per_chain must be K or (K even, J <= 10) K/2");
+    set_error("two-scale Lorenz-96: lanes_per_chain must be K, (K even, J <= 10) K/2 or (K = 6, J <= 4) 2 or 1");
     return IPMC_ERR_UNSUPPORTED;
   }
   lanes = m.dim / spl;
@@ -705,13 +754,19 @@ int l96ts_eval(const ipmc_model& m, int32_t dtype, int64_t n, const void* u, con
     return IPMC_ERR_UNSUPPORTED;
   }
   const bool fm = m.arith == IPMC_ARITH_FMA;
-  if (ts_spl(m, nullptr) == 2) {
-    if (dtype == IPMC_F64)
-      return fm ? ts_eval_t<double, true, 2>(m, n, u, y, ginv, out, phi, st)
-                : ts_eval_t<double, false, 2>(m, n, u, y, ginv, out, phi, st);
-    return fm ? ts_eval_t<float, true, 2>(m, n, u, y, ginv, out, phi, st)
-              : ts_eval_t<float, false, 2>(m, n, u, y, ginv, out, phi, st);
+  const int spl = ts_spl(m, nullptr);
+#define IPMC_TS_SPL_EVAL(P)                                                                                        \
+  if (spl == P) {                                                                                                  \
+    if (dtype == IPMC_F64)                                                                                         \
+      return fm ? ts_eval_t<double, true, P>(m, n, u, y, ginv, out, phi, st)                                       \
+                : ts_eval_t<double, false, P>(m, n, u, y, ginv, out, phi, st);                                     \
+    return fm ? ts_eval_t<float, true, P>(m, n, u, y, ginv, out, phi, st)                                          \
+              : ts_eval_t<float, false, P>(m, n, u, y, ginv, out, phi, st);                                        \
   }
+  IPMC_TS_SPL_EVAL(2)
+  IPMC_TS_SPL_EVAL(3)
+  IPMC_TS_SPL_EVAL(6)
+#undef IPMC_TS_SPL_EVAL
   if (dtype == IPMC_F64)
     return fm ? ts_eval_t<double, true, 1>(m, n, u, y, ginv, out, phi, st)
               : ts_eval_t<double, false, 1>(m, n, u, y, ginv, out, phi, st);

@@ -232,14 +232,14 @@ constexpr int kPreFactor = 4;
 constexpr int kPreLds = kPreFactor * kSpecBlock;  // steps per block (all groups)
 
 // LDS of one small_spec_kernel block: the proposal park, the linear model's
-// constants and (linear) the pre-drawn w / log r.  f64 at kSpecBlock = 256 is
+// constants and (linear) the pre-drawn w / log r, (others) the slots' w.  f64 at kSpecBlock = 256 is
 // 96 KiB -- it fits gfx950's 160 KiB per CU only (64 KiB on gfx942): a larger
 // IPMC_SPEC_BLOCK or kPreFactor has to stay under the limit.
 template <typename T, int MODEL>
 constexpr size_t small_spec_lds_bytes() {
   return sizeof(T) * (size_t)kSpecKMax * kSpecBlock + sizeof(T) * (MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1) +
-         (MODEL == IPMC_MODEL_LINEAR ? (sizeof(T) * (size_t)kPreLds * kSpecKMax + sizeof(double) * kPreLds)
-                                     : sizeof(T) + sizeof(double));
+         (MODEL == IPMC_MODEL_LINEAR ? (sizeof(T) * (size_t)kPreLds * kSpecKMax + sizeof(double) * kPreLds + sizeof(T))
+                                     : sizeof(T) + sizeof(double) + sizeof(T) * (size_t)kSpecKMax * kSpecBlock);
 }
 
 template <typename T, int MODEL, bool FM, int S>
@@ -252,6 +252,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   __shared__ T lin_c[MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1];
   __shared__ T pre_w[PRE ? kPreLds * kSpecKMax : 1];    // [group][step in chunk][j]
   __shared__ double pre_lr[PRE ? kPreLds : 1];           // [group][step in chunk]: log r
+  __shared__ T wpark[PRE ? 1 : kSpecKMax * kSpecBlock];  // accept mode: the slots' w (non-PRE)
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int sub = t & (S - 1);
@@ -334,9 +335,26 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       }
     }
   };
+  // The speculated path (results are bit-identical either way; only the steps
+  // a round settles change).  Reject mode: every slot proposes from the
+  // current state -- the path on which the next steps are rejected -- and the
+  // first acceptance ends the round.  Accept mode: slot s proposes from slot
+  // s-1's proposal -- the path on which they are accepted, each slot forming
+  // the proposals of the slots before it from their draws in the sequential
+  // order -- and the first rejection ends the round; the mismatching slot's own
+  // decision is valid (its inputs were right), so a round settles up to S
+  // steps either way.  A chain runs accept mode while it accepts at least half
+  // of this launch's steps (at its first round: its accept counter over the
+  // global steps before the launch, if any).  Config 2 accepts 88 %: reject
+  // mode settles ~1.1 steps per round there, accept mode ~1/(1-p) = 8.
+  const int64_t hist_acc = s.accepts ? s.accepts[chain] : 0;
+  const bool prior_accept = !s.accepts || s.step0 == 0 || (uint64_t)(2 * hist_acc) >= s.step0;
+  T* wown = wpark + t;                    // this lane's proposal noise, wown[j * kSpecBlock] (accept mode)
+  const T* wgroup = wpark + (t - sub);
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + sub;
+    const bool amode = st == 0 ? prior_accept : 2 * nacc >= st;
     if constexpr (PRE) {
       // refill when this round's slots reach past the held draws (uniform per group)
       if (st + S > pend && pend < s.n_steps) {
@@ -359,48 +377,54 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
         wave_sync_lds();
       }
     }
+    // this slot's proposal noise w (step tt)
+    T w[kSpecKMax];
+    if (sub < left) {
+      if constexpr (PRE) {
+        const int pi = (int)(tt - pbase);
+#pragma unroll
+        for (int j = 0; j < kSpecKMax; ++j) w[j] = gw[pi * kSpecKMax + j];
+      } else {
+        draw_w(s.step0 + (uint64_t)tt, w);
+        if (amode) {
+#pragma unroll
+          for (int j = 0; j < kSpecKMax; ++j) wown[j * kSpecBlock] = w[j];
+        }
+      }
+    }
+    // accept mode: the proposals of the slots before this one, in step order
+    T pv[kSpecKMax];
+#pragma unroll
+    for (int j = 0; j < kSpecKMax; ++j) pv[j] = ur[j];
+    if (!PRE) wave_sync_lds();  // the parked w of the group's slots
+    if (amode) {
+      const int64_t lim = left < S ? left : S;
+#pragma unroll 1
+      for (int q = 0; q < sub && q < lim; ++q) {
+        const int64_t tq = st + q;
+        const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
+        const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
+#pragma unroll
+        for (int j = 0; j < kSpecKMax; ++j) {
+          if (j < k) {
+            const T wq = PRE ? gw[(int)(tq - pbase) * kSpecKMax + j] : wgroup[j * kSpecBlock + q];
+            pv[j] = propose_one<T>(rw, pv[j], wq, cq, bq);
+          }
+        }
+      }
+    }
     bool ok = false, acc = false;
     T phv = (T)0;
+    double lr = 0.0;
     if (sub < left) {
       const uint64_t step = s.step0 + (uint64_t)tt;
       const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      double z0 = 0.0, z1 = 0.0;
       ok = true;
-      T xi[kSpecKMax];
-      if (PRE) {
-        const int pi = (int)(tt - pbase);
-#pragma unroll
-        for (int j = 0; j < kSpecKMax; ++j) {
-          if (j < k) {
-            const T vj = propose_one<T>(rw, ur[j], gw[pi * kSpecKMax + j], cs, bs);
-            v[j * kSpecBlock] = vj;
-            const T tb = vj + offr[j];
-            if (lo && !(lor[j] < tb)) ok = false;
-            if (hi && !(tb < hir[j])) ok = false;
-          }
-        }
-      } else if (chol) {
-#pragma unroll
-        for (int j = 0; j < kSpecKMax; j += 2) {
-          if (j < k) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
-          xi[j] = (T)z0;
-          xi[j + 1] = (T)z1;
-        }
-      }
 #pragma unroll
       for (int j = 0; j < kSpecKMax; ++j) {
-        if (!PRE && j < k) {
-          T w;
-          if (chol) {  // non-diagonal prior: chol_propose's order
-            w = (T)0;
-#pragma unroll
-            for (int i = 0; i <= j; ++i) w = w + xi[i] * chol[j * k + i];
-          } else {
-            if ((j & 1) == 0) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
-            w = sqr[j] * (T)((j & 1) ? z1 : z0);
-          }
-          const T vj = propose_one<T>(rw, ur[j], w, cs, bs);
+        if (j < k) {
+          const T vj = propose_one<T>(rw, pv[j], w[j], cs, bs);
           v[j * kSpecBlock] = vj;
           const T tb = vj + offr[j];  // + 0 when there is no offset: the same bits as vj
           if (lo && !(lor[j] < tb)) ok = false;
@@ -426,25 +450,42 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
           }
           phv = phv + (T)0.5 * r2;
         }
-        if constexpr (PRE) acc = (double)(phu - phv) > glr[tt - pbase];  // pcn_accept with its log r
-        else acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+        lr = PRE ? glr[tt - pbase] : det_log(accept_uniform(s.seed, gid, step));
       }
     }
+    // pcn_accept against the state this slot proposed from: the current state,
+    // or (accept mode) the previous slot's proposal
+    const T phl = __shfl(phv, (lane + 63) & 63, 64);
+    if (ok) acc = (double)(((amode && sub > 0) ? phl : phu) - phv) > lr;
     wave_sync_lds();
     const unsigned long long accm = (__ballot(acc) >> gbase) & gmask;
     const unsigned long long okm = (__ballot(ok) >> gbase) & gmask;
-    const int first = accm ? __builtin_ctzll(accm) : S;  // first accepted lane of the group
-    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
+    const int lim = (int)(left < S ? left : S);
+    int first, used, nar, win;  // first mismatching slot, steps settled, accepts, slot of the new state
+    if (!amode) {
+      first = accm ? __builtin_ctzll(accm) : S;  // first accepted slot of the group
+      used = first < S ? first + 1 : lim;
+      nar = first < S ? 1 : 0;
+      win = first < S ? first : -1;
+    } else {
+      const unsigned long long rej = ~accm & (lim >= 64 ? ~0ull : ((1ull << lim) - 1));
+      first = rej ? __builtin_ctzll(rej) : S;  // first rejected slot
+      used = first < S ? first + 1 : lim;
+      nar = first < S ? first : lim;
+      win = nar - 1;
+    }
     ncalls += __builtin_popcountll(okm & (used >= 64 ? ~0ull : ((1ull << used) - 1)));
-    const T phf = __shfl(phv, gbase + (first < S ? first : 0), 64);
+    const T phf = __shfl(phv, gbase + (win >= 0 ? win : 0), 64);
+    // the slot whose proposal is the state after step st+q (-1: the old state)
+    auto last_acc = [&](int q) { return amode ? (q < nar ? q : nar - 1) : (q == first ? first : -1); };
     if (s.sum_u && sub == 0) {
       // the states after each of the `used` steps, in step order
       for (int q = 0; q < used; ++q) {
-        const bool moved = (q == first);
+        const int la = last_acc(q);
 #pragma unroll
         for (int j = 0; j < kSpecKMax; ++j) {
           if (j < k) {
-            const double ud = moved ? (double)vgroup[j * kSpecBlock + first] : (double)ur[j];
+            const double ud = la >= 0 ? (double)vgroup[j * kSpecBlock + la] : (double)ur[j];
             s.sum_u[chain * k + j] += ud;
             if (s.sum_u2) s.sum_u2[chain * k + j] += ud * ud;
           }
@@ -454,21 +495,21 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
     if (s.sample_every > 0 && sub == 0) {
       // the samples among the `used` steps: the state after step st+q
       while (clk.next < st + used) {
-        const int q = (int)(clk.next - st);
+        const int la = last_acc((int)(clk.next - st));
         const int64_t sl = clk.take(clk.next);
         T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
 #pragma unroll
         for (int j = 0; j < kSpecKMax; ++j)
-          if (j < k) so[j] = (q == first) ? vgroup[j * kSpecBlock + first] : ur[j];
+          if (j < k) so[j] = la >= 0 ? vgroup[j * kSpecBlock + la] : ur[j];
       }
     }
-    if (first < S) {
+    if (win >= 0) {
 #pragma unroll
       for (int j = 0; j < kSpecKMax; ++j)
-        if (j < k) ur[j] = vgroup[j * kSpecBlock + first];
+        if (j < k) ur[j] = vgroup[j * kSpecBlock + win];
       phu = phf;
-      ++nacc;
     }
+    nacc += nar;
     wave_sync_lds();  // the parks are rewritten next round
     st += used;
   }

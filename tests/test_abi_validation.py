@@ -260,6 +260,8 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     mt = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=30, dim=6)
     mt.fast_per_slow = 4
     s = _sweep(n=65536)
+    assert _plan(h, mt, s) == (2, 1, 1)  # K=6 J<=4: 3 slow variables per lane, pairs of lanes (DPP halos)
+    mt.fast_per_slow = 8
     assert _plan(h, mt, s) == (6, 1, 1)
     mt = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=180, dim=36)
     mt.fast_per_slow = 10
@@ -325,3 +327,39 @@ def test_sample_every_validation(h):
     _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "sample_stride >= k")
     s.sample_stride, s.n_steps = 400, 0
     assert h.ipmc_pcn_sweep(m, C.byref(s), None) == _abi.OK  # no step, no in-launch sample: nothing to copy
+
+
+def test_sample_every_rejects_overlapping_layouts(h):
+    """With n_s = n_steps / sample_every samples per chain, a chain's samples
+    may not run into the next chain's rows ([chain, sample, k] needs
+    sample_stride >= (n_s-1)*sample_step_stride + k, [sample, chain, k] needs
+    sample_step_stride >= (n_chains-1)*sample_stride + k)."""
+    m = C.byref(_model())
+    s = _sweep(n=8)
+    s.n_steps, s.sample_every, s.sample_out = 10, 2, DUMMY
+    s.sample_stride, s.sample_step_stride = 40, 40  # the sample_every = 0 convention: overlaps
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "samples overlap")
+    s.sample_stride, s.sample_step_stride = 199, 40  # one element short of [chain, 5 samples, 40]
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "samples overlap")
+    s.sample_stride, s.sample_step_stride = 40, 319  # one element short of [5 samples, 8 chains, 40]
+    _status(h, h.ipmc_pcn_sweep(m, C.byref(s), None), _abi.ERR_INVALID, "samples overlap")
+
+
+def test_pcn_draws_and_copy_validation(h):
+    """ipmc_pcn_draws / ipmc_copy_rows_d2h (ABI 10) argument checks (no GPU call)."""
+    _status(h, h.ipmc_pcn_draws(1, 0, 4, 0, 3, 0, _abi.F64, DUMMY, None, DUMMY, None, None), _abi.ERR_INVALID,
+            "k must be positive")
+    _status(h, h.ipmc_pcn_draws(1, 0, 4, 0, 3, 2, 7, DUMMY, None, DUMMY, None, None), _abi.ERR_INVALID, "bad dtype")
+    _status(h, h.ipmc_pcn_draws(1, (1 << 32) - 2, 4, 0, 3, 2, _abi.F64, DUMMY, None, DUMMY, None, None),
+            _abi.ERR_INVALID, "2^32")
+    _status(h, h.ipmc_pcn_draws(1, 0, 4, (1 << 63) - 2, 3, 2, _abi.F64, DUMMY, None, DUMMY, None, None),
+            _abi.ERR_INVALID, "below 2^63")
+    _status(h, h.ipmc_pcn_draws(1, 0, 4, 0, 3, 2, _abi.F64, DUMMY, None, None, None, None), _abi.ERR_INVALID,
+            "w is NULL")
+    _status(h, h.ipmc_pcn_draws(1, 0, 4, 0, 3, 2, _abi.F64, None, None, DUMMY, None, None), _abi.ERR_INVALID,
+            "both NULL")
+    assert h.ipmc_pcn_draws(1, 0, 4, 0, 0, 2, _abi.F64, DUMMY, None, DUMMY, None, None) == _abi.OK  # nothing to draw
+    _status(h, h.ipmc_copy_rows_d2h(DUMMY, 8, DUMMY, 16, 16, 4, None), _abi.ERR_INVALID, "pitch < width")
+    _status(h, h.ipmc_copy_rows_d2h(None, 16, DUMMY, 16, 16, 4, None), _abi.ERR_INVALID, "NULL")
+    _status(h, h.ipmc_copy_rows_d2h(DUMMY, 16, DUMMY, 16, -1, 4, None), _abi.ERR_INVALID, "negative")
+    assert h.ipmc_copy_rows_d2h(DUMMY, 16, DUMMY, 16, 16, 0, None) == _abi.OK

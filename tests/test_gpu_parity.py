@@ -705,9 +705,11 @@ def test_burgers_every_layout_bit_exact(dev, orc, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
-    """small_spec_kernel (S lanes evaluate S consecutive steps, the first
-    acceptance ends the round) equals the sequential chain bit for bit, for
-    every width, with schedules, box constraint, sums and the RW regularizer."""
+    """small_spec_kernel (S lanes evaluate S consecutive steps; along the reject
+    path the first acceptance ends the round, along the accept path the first
+    rejection) equals the sequential chain bit for bit, for every width, with
+    schedules, box constraint, sums and the RW regularizer, at low and high
+    acceptance."""
     from ip_mcmc_amd import LinearOperator, Lorenz63Operator
 
     rng = np.random.default_rng(23)
@@ -721,13 +723,18 @@ def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
            Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=200, arith="reference")]
     n = 37
     sched = np.stack([np.linspace(0.05, 0.4, n), np.sqrt(1 - np.linspace(0.05, 0.4, n) ** 2)], axis=1)
-    for op in ops:
+    high = 0
+    for op, broad in [(o, b) for o in ops for b in (False, True)]:
         U0, phi0, y, ginv, sq = _problem(op, 45, dtype, orc, seed=2)
+        if broad:  # a broad posterior: most steps accepted, the kernel speculates along the accept path
+            ginv = ginv * 0.002
+            phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
         box = (np.full(op.k, -1.5), None, None)
         box2 = (np.full(op.k, -1.2), np.full(op.k, 1.4), np.full(op.k, 0.1))
         for kw in (dict(), dict(box=box), dict(box=box2), dict(sched=sched), dict(want_sums=True)):
             o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, **kw)
             assert 0 < o["acc"].sum() < 45 * n
+            high += o["acc"].sum() > 0.6 * 45 * n
             for w in (1, 0, 2, 8, 64):
                 d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 71, 4, n, dtype, dev, spec=w, **kw)
                 _assert_same(d, o, (type(op).__name__, op.arith, w, list(kw)))
@@ -741,6 +748,7 @@ def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
             d = _sweep_device(op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, dev, spec=w, proposal="rw",
                               reg_scale=rs)
             _assert_same(d, o, (type(op).__name__, "rw", w))
+    assert high >= 10, high  # the accept-mode path ran
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])

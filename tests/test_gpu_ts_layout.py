@@ -1,5 +1,6 @@
 """Two-scale Lorenz-96 lane layouts: one or two slow variables per lane
-(lanes_per_chain = K or K/2), with and without speculative slots, equal the
+(lanes_per_chain = K or K/2) and, for K = 6 with J <= 4, three (2 lanes, DPP
+halos) or all six (1 lane), with and without speculative slots, equal the
 oracle bit for bit (G, Φ and sweeps)."""
 import numpy as np
 import pytest
@@ -33,7 +34,10 @@ def test_ts_two_slow_per_lane_bit_exact(dev_ts, orc, dtype, K, J):
         ginv = ginv * 0.2
         phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
         o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 4, 7, 9, dtype, want_sums=True)
-        for lanes, spec in ((K, 1), (K // 2, 1), (K // 2, 0), (K, 0)):
+        layouts = [(K, 1), (K // 2, 1), (K // 2, 0), (K, 0)]
+        if K == 6 and J <= 4:
+            layouts += [(2, 1), (2, 0), (2, 4), (1, 1), (1, 0), (1, 8)]
+        for lanes, spec in layouts:
             d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 4, 7, 9, dtype, dev_ts, lanes=lanes, spec=spec,
                               want_sums=True)
             _assert_same(d, o, (K, J, arith, lanes, spec))

@@ -15,5 +15,17 @@ case "$1" in
       "cfg2:300:python tools/config_bench.py cfg2@128 cfg2g1@128 cfg2 > gpurun_out/cfg2.jsonl" \
       "stuart:400:python examples/stuart_reference.py > gpurun_out/stuart_reference.jsonl"
     ;;
+  b)  # accept-path speculation (small models) and the K=6 two-scale layouts (SPL 3 DPP pairs / 1 / 6)
+    V=ip_mcmc_amd/lib/variants
+    tools/gpu_session.sh \
+      "spec_tests:600:$PYT -q tests/test_gpu_ts_layout.py tests/test_gpu_fuzz.py tests/test_gpu_run.py tests/test_gpu_parity.py -k 'speculative or ts_ or fuzz or run or sampler' -m gpu" \
+      "cfg2:300:python tools/config_bench.py cfg2@128 cfg2g1@128 cfg2@512 > gpurun_out/cfg2_accept_mode.jsonl" \
+      "ts6_spl3:300:python tools/config_bench.py ts6 ts6@8 ts36 > gpurun_out/ts6_layouts.jsonl" \
+      "ts6_spl1:300:IPMC_LIB_PATH=$V/ts6spl1/libipmc.so python tools/config_bench.py ts6 ts6@8 >> gpurun_out/ts6_layouts.jsonl" \
+      "ts6_spl6:300:IPMC_LIB_PATH=$V/ts6spl6/libipmc.so python tools/config_bench.py ts6 ts6@8 >> gpurun_out/ts6_layouts.jsonl" \
+      "ts6_spl3b:300:python tools/config_bench.py ts6 >> gpurun_out/ts6_layouts.jsonl" \
+      "examples:300:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl" \
+      "pytest_gpu:900:$PYT tests -m gpu -q"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
