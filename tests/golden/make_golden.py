@@ -511,7 +511,16 @@ def make_dense_prior(out):
     (proposer.py:59-82: w ~ N(0, C) drawn by GaussianDistribution.sample,
     distribution.py:114-118), the draws injected as L·ξ: the linear problem of
     config 1 with an AR(1) prior, and the Lorenz-96 K=8 chain problem with a
-    periodic squared-exponential prior on the forcing field."""
+    periodic squared-exponential prior on the forcing field.
+
+    Parity scope: the reference draws w ~ N(0, C) through numpy's SVD-based
+    multivariate_normal; this harness substitutes L·ξ (L = cholesky(C), the
+    build's own draw, summed in the device's order).  These fixtures therefore
+    pin the reference's proposal arithmetic, accept rule and bookkeeping for a
+    non-diagonal prior, but NOT its sampling path: for the draws themselves
+    parity with the reference is distributional only ("parity unpinned" bit
+    for bit; tests/test_gpu_hostloop.py checks the device's L·ξ covariance
+    against C within Monte-Carlo error)."""
     g = np.array([3.0, 1.0, 4.0, 1.0])
     gamma = 0.5
     y = np.array([np.dot(g, [2.0, 7.0, 1.0, 8.0]) + 0.3])

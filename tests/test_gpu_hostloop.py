@@ -180,3 +180,26 @@ def test_stuart_example_21_composition_unchanged(dev):
     m, v = float(g[0]) * float(np.ravel(data)[0]) / denom, 1 - float(g @ g) / denom
     assert abs(samples.mean() - m) < 4 * np.sqrt(v / 400)
     assert 0.2 < accepter.ratio() < 0.9
+
+
+def test_dense_prior_draws_have_the_prior_covariance(dev):
+    """Dense priors are pinned to the reference only distributionally (the
+    reference samples N(0, C) by numpy's SVD path, the build by L·ξ;
+    tests/golden/make_golden.py:make_dense_prior): over 262 144 chains the
+    sample covariance of ipmc_pcn_draws' w equals C entrywise within 5
+    standard errors, se_ij = sqrt((C_ii C_jj + C_ij²) / n), and the mean is 0
+    within 5 se."""
+    from ip_mcmc_amd.hostloop import device_draws
+
+    k, n = 6, 262144
+    idx = np.arange(k)
+    C = 0.7 ** np.abs(idx[:, None] - idx[None, :]) * np.sqrt(np.outer(1 + idx, 1 + idx))
+    L = np.linalg.cholesky(C)
+    w, _ = device_draws(99, 0, n, 5, 1, k, np.float64, None, L, dev)
+    w = w[0]
+    mean = w.mean(axis=0)
+    assert np.all(np.abs(mean) < 5 * np.sqrt(np.diag(C) / n)), mean
+    S = np.cov(w, rowvar=False)
+    se = np.sqrt((np.outer(np.diag(C), np.diag(C)) + C**2) / n)
+    z = np.abs(S - C) / se
+    assert z.max() < 5, z.max()

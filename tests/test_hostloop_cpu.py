@@ -254,3 +254,55 @@ def test_python_potential_value_is_the_reference_formula(golden):
     pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
     vals = np.array([pot(u) for u in golden["lin_phi_u"]])
     np.testing.assert_allclose(vals, golden["lin_phi"], rtol=1e-14, atol=1e-13)
+
+
+def test_sample_file_streams_the_same_samples(odraws, golden, tmp_path):
+    """run(sample_file=...) on the host path writes an np.load-able .npy equal
+    to the in-memory samples."""
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    prior = GaussianDistribution(np.zeros(4), np.eye(4))
+    mem = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed)).run(
+        np.zeros((4, 4)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    f = str(tmp_path / "chains.npy")
+    out = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed)).run(
+        np.zeros((4, 4)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval, sample_file=f)
+    np.testing.assert_array_equal(np.asarray(out), mem)
+    np.testing.assert_array_equal(np.load(f), golden["lin_samples"])
+    one = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed)).run(
+        np.zeros(4), n_samples=n_samples, burn_in=burn_in, sample_interval=interval, sample_file=f)
+    np.testing.assert_array_equal(np.asarray(one), golden["lin_samples"][0])
+
+
+def test_float32_chains_round_like_the_kernels(odraws, orc):
+    """f32 chains on the host path: v, Φ and the accept comparison in float32
+    (the kernels' dtype rules), equal to the oracle's f32 sweep for the same
+    linear G evaluated in float32 by the caller."""
+    from ip_mcmc_amd import LinearOperator
+
+    rng = np.random.default_rng(6)
+    A = rng.normal(size=(3, 4)).astype(np.float32).astype(np.float64)
+    op = LinearOperator(A, arith="reference")
+    y = A @ np.array([0.3, -0.2, 0.5, 0.1]) + 0.1 * rng.normal(size=3)
+    ginv = np.full(3, 10.0)
+    U0 = (0.2 * rng.normal(size=(5, 4))).astype(np.float32)
+
+    def G32(u):  # G in float32, in the kernels' order: acc = 0; acc = acc + A_ij (θ0_j + u_j)
+        u32 = np.asarray(u, dtype=np.float32)
+        A32 = A.astype(np.float32)
+        acc = np.zeros(3, dtype=np.float32)
+        for j in range(4):
+            acc = acc + A32[:, j] * (np.float32(0) + u32[j])
+        return acc.astype(np.float64)
+
+    noise = GaussianDistribution(np.zeros(3), 0.01 * np.eye(3))
+    s = MCMCSampler(ConstSteppCNProposer(0.3, GaussianDistribution(np.zeros(4), np.eye(4))),
+                    CountedAccepter(pCNAccepter(EvolutionPotential(G32, y, noise))), PhiloxRNG(8), dtype=np.float32)
+    last = s.run(U0.astype(np.float64), n_samples=1, burn_in=30, sample_interval=30, keep="last")
+    Uo = U0.copy()
+    phio = orc.potential(op, Uo, y, ginv, np.float32)
+    acco = np.zeros(5, dtype=np.int64)
+    orc.pcn_sweep(op, Uo, phio, y, ginv, np.ones(4), 0.3, 8, 0, 30, accepts=acco)
+    np.testing.assert_array_equal(last, Uo.astype(np.float64))
+    np.testing.assert_array_equal(s.state.phi, phio)
+    assert np.array_equal(s.accepter.accepts, acco) and acco.sum() > 0

@@ -11,6 +11,14 @@ bench.py reports next to its own cpu_baseline (clearly labelled: measured
 here, not on the GPU box).
 
   python tools/reference_cpu_baseline.py [--procs P] [--steps S]
+  python tools/reference_cpu_baseline.py --config 1 [--samples N]
+
+--config 1 times the reference's own config-1 script composition instead
+(stuart_examples.py:58-109, example 2.1: the closure G, pCNProposer(0.25),
+CountedAccepter(pCNAccepter), scalar noise, default burn-in 1 000 and interval
+200, one chain) -> profiles/r3/reference_cpu_cfg1.json, beside
+examples/stuart_reference.py's run of the same composition through
+ip_mcmc_amd's host step.
 """
 import argparse
 import contextlib
@@ -81,11 +89,50 @@ def worker(args):
     return time.perf_counter() - t0
 
 
+def config1(n_samples):
+    import numpy as np
+
+    ip_mcmc, _ = _setup()
+    g = np.array([int(x) for x in str(np.pi) if x != "."])[:1]
+    u = np.array([int(x) for x in str(np.e) if x != "."])[:1]
+
+    def G(u):
+        return np.dot(g, u)
+
+    prior = ip_mcmc.GaussianDistribution(mean=np.zeros_like(u), covariance=np.identity(1))
+    noise = ip_mcmc.GaussianDistribution(mean=0, covariance=0.5**2)
+    rng = np.random.default_rng(1)
+    data = G(u) + noise.sample(rng)
+    acc = ip_mcmc.CountedAccepter(ip_mcmc.pCNAccepter(potential=ip_mcmc.EvolutionPotential(G, data, noise)))
+    sampler = ip_mcmc.MCMCSampler(ip_mcmc.pCNProposer(beta=0.25, prior=prior), acc, rng)
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        samples = sampler.run(u_0=np.zeros_like(u), n_samples=n_samples)
+    el = time.perf_counter() - t0
+    steps = 800 + n_samples * 200
+    rec = {"value": steps / el, "unit": "pCN steps/s", "cores": 1, "kind": "reference",
+           "sample": f"stuart_examples.py example 2.1 as composed there, one chain, n_samples={n_samples} "
+                     f"({steps} pCN steps), reference MCMCSampler on numpy/scipy",
+           "accept_ratio": float(acc.ratio()), "sample_mean": float(samples.mean()), "wall_s": el,
+           "host": platform.processor() or platform.machine(),
+           "measured_on": "build container (the reference does not exist on the GPU box)"}
+    out = os.path.join(REPO, "profiles", "r3", "reference_cpu_cfg1.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=len(os.sched_getaffinity(0)))
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--samples", type=int, default=500)
     args = ap.parse_args()
+    if args.config == 1:
+        config1(args.samples)
+        return
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(args.procs) as pool:
         times = pool.map(worker, [(i, args.steps) for i in range(args.procs)])

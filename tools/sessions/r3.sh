@@ -4,6 +4,8 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 PYT="python -u -m pytest -p no:cacheprovider --timeout 120 --timeout-method thread -rf"
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+B="python bench.py --steps 5 --warmup 1 --no-cpu --no-extra"
 case "$1" in
   a)  # host loop, FMA-vs-reference, full-size configs, bench plumbing; then everything
     tools/gpu_session.sh \
@@ -24,8 +26,23 @@ case "$1" in
       "ts6_spl1:300:IPMC_LIB_PATH=$V/ts6spl1/libipmc.so python tools/config_bench.py ts6 ts6@8 >> gpurun_out/ts6_layouts.jsonl" \
       "ts6_spl6:300:IPMC_LIB_PATH=$V/ts6spl6/libipmc.so python tools/config_bench.py ts6 ts6@8 >> gpurun_out/ts6_layouts.jsonl" \
       "ts6_spl3b:300:python tools/config_bench.py ts6 >> gpurun_out/ts6_layouts.jsonl" \
+      "sq_cfg2:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_cfg2 -o run -- python tools/config_bench.py cfg2@128" \
+      "sq_ts6:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_ts6 -o run -- python tools/config_bench.py ts6" \
       "examples:300:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl" \
       "pytest_gpu:900:$PYT tests -m gpu -q"
+    ;;
+  c)  # the published line and its profiles from one box: bench, rocprofv3 --stats of the same
+      # command, the three PMC passes (HBM bytes, clock, VALU issue) of the headline kernel
+    tools/gpu_session.sh \
+      "bench:400:python bench.py > gpurun_out/bench_line.json" \
+      "stats:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats -o run -- python bench.py --no-cpu" \
+      "fetch64:200:timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc64/fetch -o run -- $B" \
+      "write64:200:timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc64/write -o run -- $B" \
+      "sq64:200:timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc64/sq -o run -- $B" \
+      "fetch32:200:timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc32/fetch -o run -- $B --dtype f32" \
+      "write32:200:timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc32/write -o run -- $B --dtype f32" \
+      "sq32:200:timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc32/sq -o run -- $B --dtype f32" \
+      "summ:60:python tools/pmc_summarize.py gpurun_out/pmc64 f64 65536 gpurun_out/pmc_l96_f64.json && python tools/pmc_summarize.py gpurun_out/pmc32 f32 65536 gpurun_out/pmc_l96_f32.json"
     ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
