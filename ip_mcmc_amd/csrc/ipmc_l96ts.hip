@@ -512,19 +512,37 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
+  const bool prior = spec_accept_prior(s, chain);
+  const T* chol = (const T*)s.prior_chol;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + slot;
+    const bool amode = S > 1 && spec_accept_mode(st, nacc, prior);
     int kq = c.sub;
     asm volatile("" : "+v"(kq));
     bool ok = false, acc = false;
     T phv = (T)0;
+    double lr = 0.0;
     T v[3] = {(T)0, (T)0, (T)0};
     if (slot < left) {  // uniform per slot
+      // the state this slot proposes from: the chain's, or (accept mode) the
+      // proposals of the slots before it, formed from their draws in step order
+      T pv[3] = {ur[0], ur[1], ur[2]};
+      if (amode) {
+        for (int q = 0; q < slot; ++q) {
+          const int64_t tq = st + q;
+          const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
+          const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
+          T nv[3];
+          pcn_propose<T, 3>(pv, sq, cq, bq, s.seed, gid, s.step0 + (uint64_t)tq, 0, nv, rw, chol, 3);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) pv[j] = nv[j];
+        }
+      }
       const uint64_t step = s.step0 + (uint64_t)tt;
       const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, rw, (const T*)s.prior_chol, 3);
+      pcn_propose<T, 3>(pv, sq, cs, bs, s.seed, gid, step, 0, v, rw, chol, 3);
       ok = true;
       if (s.box_lo || s.box_hi) {
         const T* lo = (const T*)s.box_lo;
@@ -540,49 +558,80 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
       if (ok) {
         phv = ts_phi<T, J, FM, SPL>(m, v, c, kq, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
         if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
-        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+        lr = det_log(accept_uniform(s.seed, gid, step));
       }
     }
+    // pcn_accept against the state this slot proposed from (accept mode: the
+    // previous slot's proposal, whose Φ its lanes hold)
+    const T phl = __shfl(phv, cbase + (slot > 0 ? slot - 1 : 0) * L, 64);
+    if (ok) acc = (double)(((amode && slot > 0) ? phl : phu) - phv) > lr;
     // one bit per slot (its first lane, at bit slot*L of the chain's lanes)
     const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
     const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
     const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-    const int first = accm ? __builtin_ctzll(accm) / L : S;
-    const int used = first < S ? first + 1 : (int)(left < S ? left : S);
-    const int ubits = used * L;
+    const SpecRound rd = spec_round(amode, accm, S, L, left);
+    const int ubits = rd.used * L;
     ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-    const int wl = cbase + (first < S ? first : 0) * L;  // the winning slot's first lane
+    // every slot's proposal is needed for the recorded states of an accept-mode round
+    const int wl = cbase + (rd.win >= 0 ? rd.win : 0) * L;  // the winning slot's first lane
     T vf[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
     const T phf = __shfl(phv, wl, 64);
-    if (s.sum_u && r == 0) {
-      for (int qq = 0; qq < used; ++qq) {
+    if ((s.sum_u || s.sample_every > 0) && amode) {
+      // recorded states of an accept-mode round: slot q's proposal for q < nar,
+      // gathered by every lane (uniform loop), written by lane r == 0
+      for (int q = 0; q < rd.used; ++q) {
+        const int la = spec_last_acc(rd, amode, q);
+        T vq[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double ud = (qq == first) ? (double)vf[j] : (double)ur[j];
-          s.sum_u[chain * 3 + j] += ud;
-          if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+        for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * L, 64);
+        if (r == 0) {
+          if (s.sum_u) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const double ud = la >= 0 ? (double)vq[j] : (double)ur[j];
+              s.sum_u[chain * 3 + j] += ud;
+              if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+            }
+          }
+          if (s.sample_every > 0 && clk.next == st + q) {
+            const int64_t sl = clk.take(clk.next);
+            T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) so[j] = la >= 0 ? vq[j] : ur[j];
+          }
+        }
+      }
+    } else {
+      if (s.sum_u && r == 0) {
+        for (int qq = 0; qq < rd.used; ++qq) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const double ud = (qq == rd.first) ? (double)vf[j] : (double)ur[j];
+            s.sum_u[chain * 3 + j] += ud;
+            if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+          }
+        }
+      }
+      if (s.sample_every > 0 && r == 0) {
+        // the samples among the `used` steps: the state after step st+qq
+        while (clk.next < st + rd.used) {
+          const int qq = (int)(clk.next - st);
+          const int64_t sl = clk.take(clk.next);
+          T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) so[j] = (qq == rd.first) ? vf[j] : ur[j];
         }
       }
     }
-    if (s.sample_every > 0 && r == 0) {
-      // the samples among the `used` steps: the state after step st+qq
-      while (clk.next < st + used) {
-        const int qq = (int)(clk.next - st);
-        const int64_t sl = clk.take(clk.next);
-        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) so[j] = (qq == first) ? vf[j] : ur[j];
-      }
-    }
-    if (first < S) {
+    if (rd.win >= 0) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) ur[j] = vf[j];
       phu = phf;
-      ++nacc;
     }
-    st += used;
+    nacc += rd.nar;
+    st += rd.used;
   }
   if (r == 0) {
     phi[chain] = phu;

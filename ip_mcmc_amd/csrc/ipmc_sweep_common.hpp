@@ -176,6 +176,58 @@ struct SampleClock {
   }
 };
 
+// ---------------------------------------------------------- speculation
+// A speculative round evaluates the next S steps of a chain at once, slot s
+// taking step st+s under a guess of the decisions before it: reject mode (the
+// steps before it rejected: every slot proposes from the current state, the
+// first acceptance ends the round) or accept mode (accepted: slot s proposes
+// from slot s-1's proposal, the first rejection ends the round).  The slot
+// where the guess first fails still decided correctly (its inputs were
+// right), so a round settles `used` steps either way and the results are
+// bit-identical to the sequential chain; the guess only changes how many.  A
+// chain guesses "accept" while it accepts at least half of this launch's
+// steps; before its first round, `prior`.
+__device__ __forceinline__ bool spec_accept_mode(int64_t st, int64_t nacc, bool prior) {
+  return st == 0 ? prior : 2 * nacc >= st;
+}
+// The prior at a launch's first round: the chain's accept counter over the
+// global steps before the launch (accept mode without any history).
+__device__ __forceinline__ bool spec_accept_prior(const ipmc_sweep& s, int64_t chain) {
+  if (!s.accepts || s.step0 == 0) return true;
+  return (uint64_t)(2 * s.accepts[chain]) >= s.step0;
+}
+
+struct SpecRound {
+  int first;  // the first slot whose guess failed (S: none)
+  int used;   // steps settled by the round
+  int nar;    // accepted steps among them
+  int win;    // the slot whose proposal is the chain's new state (-1: unchanged)
+};
+// From the slots' decisions: slot s's at bit s*L of acc_bits (L lanes per slot).
+__device__ __forceinline__ SpecRound spec_round(bool amode, unsigned long long acc_bits, int S, int L, int64_t left) {
+  const int lim = left < S ? (int)left : S;
+  SpecRound r;
+  if (!amode) {
+    r.first = acc_bits ? __builtin_ctzll(acc_bits) / L : S;
+    r.used = r.first < S ? r.first + 1 : lim;
+    r.nar = r.first < S ? 1 : 0;
+    r.win = r.first < S ? r.first : -1;
+  } else {
+    unsigned long long ev = 0;  // the evaluated slots' bits
+    for (int q = 0; q < lim; ++q) ev |= 1ull << (q * L);
+    const unsigned long long rej = ev & ~acc_bits;
+    r.first = rej ? __builtin_ctzll(rej) / L : S;
+    r.used = r.first < S ? r.first + 1 : lim;
+    r.nar = r.first < S ? r.first : lim;
+    r.win = r.nar - 1;
+  }
+  return r;
+}
+// The slot whose proposal is the chain's state after step st+q of the round (-1: the old state).
+__device__ __forceinline__ int spec_last_acc(const SpecRound& r, bool amode, int q) {
+  return amode ? (q < r.nar ? q : r.nar - 1) : (q == r.first ? r.first : -1);
+}
+
 // accept iff Φ(u) − Φ(v) > log r   ⇔ exp(Φ(u) − Φ(v)) > r   (accepter.py:62, 121-122)
 template <typename T>
 __device__ __forceinline__ bool pcn_accept(T phu, T phv, uint64_t seed, uint64_t gid, uint64_t step) {

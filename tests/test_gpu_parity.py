@@ -803,13 +803,17 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
         op = BurgersOperator(N=N, dt_mode="cfl", T=0.2, arith=arith)
         # the last width spans a whole block (256 lanes: 16 slots of 16 lanes, 8 of 32)
         cases.append((op, (0, 2, 4, 16) if N == 128 else (0, 2, 8)))
-    for op, widths in cases:
+    high = 0
+    for (op, widths), scale in [(c, sc) for c in cases for sc in (0.2, 0.004)]:
         U0, phi0, y, ginv, sq = _problem(op, 19, dtype, orc, seed=3)
-        ginv = ginv * 0.2  # broad enough for acceptances inside the rounds
+        # 0.2: broad enough for acceptances inside the rounds; 0.004: most steps
+        # accepted (the two-scale kernel then speculates along the accept path)
+        ginv = ginv * scale
         phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
         for kw in (dict(), dict(box=(np.full(3, -0.3), None, None), sched=sched), dict(want_sums=True)):
             o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 8, 2**32 - 3, n, dtype, **kw)
             assert 0 < o["acc"].sum() < 19 * n, (type(op).__name__, o["acc"].sum())
+            high += isinstance(op, TwoScaleLorenz96Operator) and o["acc"].sum() > 0.6 * 19 * n
             for w in widths:
                 d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 8, 2**32 - 3, n, dtype, dev, spec=w, **kw)
                 _assert_same(d, o, (type(op).__name__, op.arith, w, list(kw)))
@@ -822,6 +826,7 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
         d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, spec=widths[-1], proposal="rw",
                           reg_scale=rs)
         _assert_same(d, o, (type(op).__name__, "rw"))
+    assert high >= 3, high  # the two-scale accept-path rounds ran
 
 
 # ------------------------------------------------ non-diagonal priors (L·ξ)
