@@ -434,7 +434,8 @@ constexpr int kBurQMax = 64;
 // <= 64, or = kBurBlock: one chain per block, its slots on the block's waves,
 // combined through LDS): slot s evaluates step st+s from the current state as
 // if the steps before it in the round were rejected; the first accepting slot
-// ends the round (see small_spec_kernel) -- bit-identical to S = 1.
+// ends the round -- or, for chains accepting most steps, along the accept path
+// (SpecRound, ipmc_sweep_common.hpp) -- bit-identical to S = 1.
 template <typename T, int CPL, int GS, bool FM>
 __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
   __shared__ T lds[kBurBlock * CPL];
@@ -461,18 +462,36 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
+  const bool prior = spec_accept_prior(s, chain);  // the speculated path (ipmc_sweep_common.hpp)
+  const bool rw = s.proposal == IPMC_PROPOSAL_RW;
+  const T* chol = (const T*)s.prior_chol;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + slot;
-    bool ok = false, acc = false;
+    const bool amode = S > 1 && spec_accept_mode(st, nacc, prior);
+    bool ok = false;
     T phv = (T)0;
+    double lr = 0.0;
     T v[3] = {(T)0, (T)0, (T)0};
     if (slot < left) {  // uniform per slot
+      // the state this slot proposes from: the chain's, or (accept mode) the
+      // proposals of the slots before it, formed from their draws in step order
+      T pv[3] = {ur[0], ur[1], ur[2]};
+      if (amode) {
+        for (int q = 0; q < slot; ++q) {
+          const int64_t tq = st + q;
+          const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
+          const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
+          T nv[3];
+          pcn_propose<T, 3>(pv, sq, cq, bq, s.seed, gid, s.step0 + (uint64_t)tq, 0, nv, rw, chol, 3);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) pv[j] = nv[j];
+        }
+      }
       const uint64_t step = s.step0 + (uint64_t)tt;
       const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      pcn_propose<T, 3>(ur, sq, cs, bs, s.seed, gid, step, 0, v, s.proposal == IPMC_PROPOSAL_RW,
-                        (const T*)s.prior_chol, 3);
+      pcn_propose<T, 3>(pv, sq, cs, bs, s.seed, gid, step, 0, v, rw, chol, 3);
       ok = true;
       if (s.box_lo || s.box_hi) {
         const T* lo = (const T*)s.box_lo;
@@ -489,23 +508,33 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
         phv = burgers_phi<T, CPL, GS, FM>(m, v, c, row, (const T*)s.y, (const T*)s.gamma_inv, nullptr);
         phv = __shfl(phv, lane & ~(GS - 1), 64);
         if (s.reg_scale) phv = phv + regularizer<T, 3, 1, FM>((const T*)s.reg_scale, v, lane);
-        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+        lr = det_log(accept_uniform(s.seed, gid, step));
       }
     }
+    // pcn_accept against the state this slot proposed from (accept mode: the
+    // previous slot's proposal, whose Φ its lanes hold)
+    T phl;
+    if (G <= 64) {
+      phl = __shfl(phv, cbase + (slot > 0 ? slot - 1 : 0) * GS, 64);
+    } else {
+      const int t = threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) vpk[j][t] = v[j];
+      vpk[3][t] = phv;
+      __syncthreads();
+      phl = vpk[3][(slot > 0 ? slot - 1 : 0) * GS];
+    }
+    const bool acc = ok && (double)(((amode && slot > 0) ? phl : phu) - phv) > lr;
     // one bit per slot (its first lane, bit slot*GS of the chain's lanes)
-    int first, used;
-    T vf[3], phf;
+    SpecRound rd;
+    T phf;
     if (G <= 64) {
       const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
       const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-      first = accm ? __builtin_ctzll(accm) / GS : S;
-      used = first < S ? first + 1 : (int)(left < S ? left : S);
-      const int ubits = used * GS;
+      rd = spec_round(amode, accm, S, GS, left);
+      const int ubits = rd.used * GS;
       ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-      const int wl = cbase + (first < S ? first : 0) * GS;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
-      phf = __shfl(phv, wl, 64);
+      phf = __shfl(phv, cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
     } else {
       const int t = threadIdx.x;
       const unsigned long long ab = __ballot(acc && c.sub == 0), ob = __ballot(ok && c.sub == 0);
@@ -513,53 +542,74 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
         bmask[0][t >> 6] = ab;
         bmask[1][t >> 6] = ob;
       }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) vpk[j][t] = v[j];
-      vpk[3][t] = phv;
       __syncthreads();
-      first = S;
-      for (int w = kBurBlock / 64 - 1; w >= 0; --w)  // the lowest accepting slot
-        if (bmask[0][w]) first = (w * 64 + __builtin_ctzll(bmask[0][w])) / GS;
-      used = first < S ? first + 1 : (int)(left < S ? left : S);
-      const int ubits = used * GS;
+      rd.first = S;  // the first slot whose guess failed
+      const int lim = left < S ? (int)left : S;
+      for (int w = kBurBlock / 64 - 1; w >= 0; --w) {
+        unsigned long long b = bmask[0][w];
+        if (amode) {  // the first rejection among the evaluated slots
+          unsigned long long ev = 0;
+          for (int i = 0; i < 64; i += GS)
+            if ((w * 64 + i) / GS < lim) ev |= 1ull << i;
+          b = ev & ~b;
+        }
+        if (b) rd.first = (w * 64 + __builtin_ctzll(b)) / GS;
+      }
+      rd.used = rd.first < S ? rd.first + 1 : lim;
+      rd.nar = amode ? (rd.first < S ? rd.first : lim) : (rd.first < S ? 1 : 0);
+      rd.win = amode ? rd.nar - 1 : (rd.first < S ? rd.first : -1);
+      const int ubits = rd.used * GS;
 #pragma unroll
       for (int w = 0; w < kBurBlock / 64; ++w) {
         const int nb = ubits - w * 64;
         if (nb > 0) ncalls += __builtin_popcountll(bmask[1][w] & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
       }
-      const int wl = (first < S ? first : 0) * GS;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) vf[j] = vpk[j][wl];
-      phf = vpk[3][wl];
-      __syncthreads();  // bmask / vpk are rewritten next round
+      phf = vpk[3][(rd.win >= 0 ? rd.win : 0) * GS];
     }
-    if (s.sum_u && r == 0) {
-      for (int q = 0; q < used; ++q) {
+    // the proposal of slot q (every lane of the chain runs this, uniform per chain)
+    auto slot_v = [&](int q, T (&out)[3]) {
+      if (G <= 64) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const double ud = (q == first) ? (double)vf[j] : (double)ur[j];
-          s.sum_u[chain * 3 + j] += ud;
-          if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+        for (int j = 0; j < 3; ++j) out[j] = __shfl(v[j], cbase + q * GS, 64);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) out[j] = vpk[j][q * GS];
+      }
+    };
+    T vf[3];
+    slot_v(rd.win >= 0 ? rd.win : 0, vf);
+    if (s.sum_u || s.sample_every > 0) {
+      for (int q = 0; q < rd.used; ++q) {
+        const int la = spec_last_acc(rd, amode, q);
+        T vq[3];
+        slot_v(la >= 0 ? la : 0, vq);
+        if (r == 0) {
+          if (s.sum_u) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              const double ud = la >= 0 ? (double)vq[j] : (double)ur[j];
+              s.sum_u[chain * 3 + j] += ud;
+              if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
+            }
+          }
+          if (s.sample_every > 0 && clk.next == st + q) {
+            // the state after step st+q is a sample
+            const int64_t sl = clk.take(clk.next);
+            T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) so[j] = la >= 0 ? vq[j] : ur[j];
+          }
         }
       }
     }
-    if (s.sample_every > 0 && r == 0) {
-      // the samples among the `used` steps: the state after step st+q
-      while (clk.next < st + used) {
-        const int q = (int)(clk.next - st);
-        const int64_t sl = clk.take(clk.next);
-        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) so[j] = (q == first) ? vf[j] : ur[j];
-      }
-    }
-    if (first < S) {
+    if (G > 64) __syncthreads();  // bmask / vpk are rewritten next round
+    if (rd.win >= 0) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) ur[j] = vf[j];
       phu = phf;
-      ++nacc;
     }
-    st += used;
+    nacc += rd.nar;
+    st += rd.used;
   }
   if (r == 0) {
     phi[chain] = phu;

@@ -259,9 +259,12 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
 // small_spec_kernel, ipmc_small.hpp): S slots of LPC lanes per chain
 // (S*LPC <= 64, one wavefront); slot s evaluates step st+s from the current
 // state -- exactly the proposal the sequential chain makes there if steps
-// st .. st+s-1 are rejected -- and the first accepting slot ends the round.
-// The state lives in registers of every slot (ur) and moves through the LDS
-// park on acceptance.  Bit-identical to l96_sweep_kernel.
+// st .. st+s-1 are rejected -- and the first accepting slot ends the round;
+// or, for chains accepting most steps, along the accept path (slot s proposes
+// from slot s-1's proposal, the first rejection ends the round; SpecRound in
+// ipmc_sweep_common.hpp).  The state lives in registers of every slot (ur)
+// and moves through the LDS park on acceptance.  Bit-identical to
+// l96_sweep_kernel.
 template <typename T, int D, int LPC, bool FM>
 __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
   constexpr int M = D / LPC;
@@ -295,19 +298,39 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
+  const bool prior = spec_accept_prior(s, chain);  // the speculated path (ipmc_sweep_common.hpp)
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + slot;
-    bool ok = false, acc = false;
+    const bool amode = spec_accept_mode(st, nacc, prior);
+    bool ok = false;
     T phv = (T)0;
+    double lr = 0.0;
     int cl = c0;
     asm volatile("" : "+v"(cl));
     if (slot < left) {  // uniform per slot
+      // the state this slot proposes from: the chain's, or (accept mode) the
+      // proposals of the slots before it, formed from their draws in step order
+      T pv[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) pv[j] = ur[j];
+      if (amode) {
+        for (int q = 0; q < slot; ++q) {
+          const int64_t tq = st + q;
+          const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
+          const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
+          T nv[M];
+          pcn_propose<T, M>(pv, (const T*)s.prior_sqrt + cl, cq, bq, s.seed, gid, s.step0 + (uint64_t)tq, c0, nv, rw,
+                            (const T*)s.prior_chol, D);
+#pragma unroll
+          for (int j = 0; j < M; ++j) pv[j] = nv[j];
+        }
+      }
       const uint64_t step = s.step0 + (uint64_t)tt;
       const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
       T v[M];
-      pcn_propose<T, M>(ur, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw,
+      pcn_propose<T, M>(pv, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw,
                         (const T*)s.prior_chol, D);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][t] = v[j];
@@ -319,49 +342,71 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
         phv = l96_potential<T, M, LPC, FM>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
                                            (const T*)s.gamma_inv + cl, h, m.n_steps, lane, stage);
         if (s.reg_scale) phv = phv + reg;
-        acc = pcn_accept<T>(phu, phv, s.seed, gid, step);
+        lr = det_log(accept_uniform(s.seed, gid, step));
       }
     }
+    // pcn_accept against the state this slot proposed from (accept mode: the
+    // previous slot's proposal, whose Φ its lanes hold)
+    T phl;
+    if (G <= 64) {
+      phl = __shfl(phv, gbase + (slot > 0 ? slot - 1 : 0) * LPC, 64);
+    } else {
+      phpark[t] = phv;
+      __syncthreads();
+      phl = phpark[(slot > 0 ? slot - 1 : 0) * LPC];
+    }
+    const bool acc = ok && (double)(((amode && slot > 0) ? phl : phu) - phv) > lr;
     // one bit per slot: the slot's lane sub == 0, at bit slot*LPC
-    int first, used;
+    SpecRound rd;
     T phf;
     if (G <= 64) {
       wave_sync_lds();
       const unsigned long long accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
       const unsigned long long okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
-      first = accm ? __builtin_ctzll(accm) / LPC : S;
-      used = first < S ? first + 1 : (int)(left < S ? left : S);
-      const int ubits = used * LPC;
+      rd = spec_round(amode, accm, S, LPC, left);
+      const int ubits = rd.used * LPC;
       ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-      phf = __shfl(phv, gbase + (first < S ? first : 0) * LPC, 64);
+      phf = __shfl(phv, gbase + (rd.win >= 0 ? rd.win : 0) * LPC, 64);
     } else {
       const unsigned long long ab = __ballot(acc && sub == 0), ob = __ballot(ok && sub == 0);
       if (lane == 0) {
         wmask[0][t >> 6] = ab;
         wmask[1][t >> 6] = ob;
       }
-      phpark[t] = phv;
       __syncthreads();
-      first = S;
-      for (int w = kL96Block / 64 - 1; w >= 0; --w)  // the lowest accepting slot
-        if (wmask[0][w]) first = (w * 64 + __builtin_ctzll(wmask[0][w])) / LPC;
-      used = first < S ? first + 1 : (int)(left < S ? left : S);
-      const int ubits = used * LPC;  // the lanes of the used slots: bits [0, ubits) of the block
+      rd.first = S;  // the first slot whose guess failed
+      const int lim = left < S ? (int)left : S;
+      for (int w = kL96Block / 64 - 1; w >= 0; --w) {
+        // slot bits of wave w: accept mode looks for the first rejection among the evaluated slots
+        unsigned long long b = wmask[0][w];
+        if (amode) {
+          unsigned long long ev = 0;
+          for (int i = 0; i < 64; i += LPC)
+            if ((w * 64 + i) / LPC < lim) ev |= 1ull << i;
+          b = ev & ~b;
+        }
+        if (b) rd.first = (w * 64 + __builtin_ctzll(b)) / LPC;
+      }
+      rd.used = rd.first < S ? rd.first + 1 : lim;
+      rd.nar = amode ? (rd.first < S ? rd.first : lim) : (rd.first < S ? 1 : 0);
+      rd.win = amode ? rd.nar - 1 : (rd.first < S ? rd.first : -1);
+      const int ubits = rd.used * LPC;  // the lanes of the used slots: bits [0, ubits) of the block
 #pragma unroll
       for (int w = 0; w < kL96Block / 64; ++w) {
         const int nb = ubits - w * 64;
         if (nb > 0) ncalls += __builtin_popcountll(wmask[1][w] & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
       }
-      phf = phpark[(first < S ? first : 0) * LPC];
+      phf = phpark[(rd.win >= 0 ? rd.win : 0) * LPC];
     }
-    const int win = t - r + (first < S ? first : 0) * LPC + sub;  // the winning slot's lane for my components
+    const int lane0 = t - r + sub;  // slot 0's lane for my components
     if (s.sum_u && slot == 0) {
       double* su = s.sum_u + chain * D + c0;
       double* su2 = s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr;
-      for (int q = 0; q < used; ++q) {
+      for (int q = 0; q < rd.used; ++q) {
+        const int la = spec_last_acc(rd, amode, q);
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-          const double ud = (q == first) ? (double)vpark[j][win] : (double)ur[j];
+          const double ud = la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j];
           su[j] += ud;
           if (su2) su2[j] += ud * ud;
         }
@@ -369,23 +414,23 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
     }
     if (s.sample_every > 0 && slot == 0) {
       // the samples among the `used` steps: the state after step st+q
-      while (clk.next < st + used) {
-        const int q = (int)(clk.next - st);
+      while (clk.next < st + rd.used) {
+        const int la = spec_last_acc(rd, amode, (int)(clk.next - st));
         const int64_t sl = clk.take(clk.next);
         T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
 #pragma unroll
-        for (int j = 0; j < M; ++j) so[j] = (q == first) ? vpark[j][win] : ur[j];
+        for (int j = 0; j < M; ++j) so[j] = la >= 0 ? vpark[j][lane0 + la * LPC] : ur[j];
       }
     }
-    if (first < S) {
+    if (rd.win >= 0) {
 #pragma unroll
-      for (int j = 0; j < M; ++j) ur[j] = vpark[j][win];
+      for (int j = 0; j < M; ++j) ur[j] = vpark[j][lane0 + rd.win * LPC];
       phu = phf;
-      ++nacc;
     }
+    nacc += rd.nar;
     if (G <= 64) wave_sync_lds();  // the parks are rewritten next round
     else __syncthreads();
-    st += used;
+    st += rd.used;
   }
   if (slot == 0) {
 #pragma unroll

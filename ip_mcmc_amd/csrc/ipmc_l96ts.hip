@@ -690,7 +690,13 @@ static int ts_spl(const ipmc_model& m, const ipmc_sweep* s) {
     if (six_ok && s->lanes_per_chain == 1) return 6;
     return -1;
   }
-  if (six_ok) return IPMC_TS6_SPL;
+  // K = 6 pairs of lanes for ensembles that fill the GPU by themselves (>= 32 768
+  // chains = one wave per SIMD of pairs) or one-step launches; a smaller
+  // ensemble's multi-step launch speculates, and its rounds are latency chains:
+  // 6 lanes per chain (5 values per lane instead of 15) and up to 10 slots --
+  // the reference's K=6 J=4 study with 1 024 chains ran 1.46x slower on pairs
+  // (profiles/r3/example_lorenz_thesis.json vs profiles/r2).
+  if (six_ok && (!s || s->n_steps <= 1 || s->n_chains >= 32768)) return IPMC_TS6_SPL;
   return (two_ok && K > 32) ? 2 : 1;
 }
 

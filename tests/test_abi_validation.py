@@ -261,6 +261,9 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     mt.fast_per_slow = 4
     s = _sweep(n=65536)
     assert _plan(h, mt, s) == (2, 1, 1)  # K=6 J<=4: 3 slow variables per lane, pairs of lanes (DPP halos)
+    s2 = _sweep(n=1024)
+    s2.n_steps = 16
+    assert _plan(h, mt, s2) == (6, 1, 10)  # a small ensemble speculates on 6 lanes per chain (latency)
     mt.fast_per_slow = 8
     assert _plan(h, mt, s) == (6, 1, 1)
     mt = _model(kind=_abi.MODEL_LORENZ96_2S, k=3, q=180, dim=36)

@@ -31,6 +31,19 @@ case "$1" in
       "examples:300:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl" \
       "pytest_gpu:900:$PYT tests -m gpu -q"
     ;;
+  d)  # the fixed tests; strong-scaling shards: speculative layouts filling 1 vs 2 waves per SIMD
+    tools/gpu_session.sh \
+      "spec_tests:600:$PYT -q tests/test_gpu_run.py tests/test_gpu_parity.py -k 'speculative or run' -m gpu" \
+      "shards:500:python tools/config_bench.py l96x65536 l96x32768@2 l96x32768@2:2~2 l96x16384@4 l96x16384@4:2~4 l96x16384@4:4~2 l96x8192@8 l96x8192@8:2~8 l96x8192@8:2~4 l96x8192@8:4~4 l96x8192@16:2~8 > gpurun_out/shards.jsonl" \
+      "cfg2:300:python tools/config_bench.py cfg2@1024 cfg2@1024~32 cfg2@1024~8 > gpurun_out/cfg2_1024.jsonl" \
+      "sq_cfg2:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_cfg2_1024 -o run -- python tools/config_bench.py cfg2@1024"
+    ;;
+  e)  # accept-path speculation in every kernel family: the parity suite, configs and the reference studies
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "configs:500:python tools/config_bench.py cfg2@1024 cfg4 cfg4visc cfg4cfl cfg4full cfg5 ts6 ts36 l96x1@256 l96x64@256 l96x1024@64 l96x8192@8 > gpurun_out/configs.jsonl" \
+      "examples:400:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/burgers_beta.py > gpurun_out/example_burgers_beta.jsonl && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl"
+    ;;
   c)  # the published line and its profiles from one box: bench, rocprofv3 --stats of the same
       # command, the three PMC passes (HBM bytes, clock, VALU issue) of the headline kernel
     tools/gpu_session.sh \
