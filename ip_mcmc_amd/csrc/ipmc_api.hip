@@ -177,8 +177,19 @@ static int l96_plan(const ipmc_model& m, const ipmc_sweep& s, int& lpc, int& cpl
         const int d = l96_dpp_lpc(m.dim, s.dtype, 1);
         if (d) l = d;
       }
+      // an ensemble that fills at least a quarter wave per SIMD on its own (a
+      // strong-scaled shard of the headline: 4 096 - 32 767 chains) speculates
+      // up to two waves per SIMD, in fp64 on the full ensemble's 2-lane layout:
+      // d=40, 8 192 chains x 8 steps per launch, 19.6 -> 20.2 M steps/s (fp64, 2
+      // lanes x 8 slots), 24.0 -> 25.4 M (fp32, 4 lanes x 4 slots); 16 384
+      // chains 19.6 -> 20.5 M / 24.1 -> 25.4 M (profiles/r3/shards.jsonl)
+      int64_t cap = 65536;
+      if (s.n_chains < 32768 && s.n_chains * (int64_t)l >= 16384) {
+        cap = 131072;
+        if (!s.lanes_per_chain && s.dtype == IPMC_F64 && m.dim % 2 == 0 && l96_has(m.dim, s.dtype, 2, 1)) l = 2;
+      }
       int w = 1;
-      while (w * 2 * l <= 64 && s.n_chains * (int64_t)l * w * 2 <= 65536) w *= 2;
+      while (w * 2 * l <= 64 && s.n_chains * (int64_t)l * w * 2 <= cap) w *= 2;
       // a whole block of slots per chain (4 waves on the CU's 4 SIMDs) while
       // the ensemble stays within one wave per SIMD
       if (w * l == 64 && s.n_chains * (int64_t)kL96SpecBlockLanes <= 65536) w = kL96SpecBlockLanes / l;

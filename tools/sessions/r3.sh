@@ -44,6 +44,12 @@ case "$1" in
       "configs:500:python tools/config_bench.py cfg2@1024 cfg4 cfg4visc cfg4cfl cfg4full cfg5 ts6 ts36 l96x1@256 l96x64@256 l96x1024@64 l96x8192@8 > gpurun_out/configs.jsonl" \
       "examples:400:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/burgers_beta.py > gpurun_out/example_burgers_beta.jsonl && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl"
     ;;
+  f)  # shard speculation cap (two waves per SIMD), the parity suite, then the shard sizes again
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "shards:500:python tools/config_bench.py l96x65536 l96x32768@2 l96x16384@4 l96x8192@8 l96x4096@16 l96x2048@16 > gpurun_out/shards_rule.jsonl" \
+      "bench8:300:python bench.py --chains 8192 --no-cpu > gpurun_out/bench_8192.json"
+    ;;
   c)  # the published line and its profiles from one box: bench, rocprofv3 --stats of the same
       # command, the three PMC passes (HBM bytes, clock, VALU issue) of the headline kernel
     tools/gpu_session.sh \
