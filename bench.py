@@ -68,7 +68,8 @@ def problem():
 
 
 class Workload:
-    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0, d=D, chains_per_lane=0, per_launch=1):
+    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0, d=D, chains_per_lane=0, per_launch=1,
+                 spec_width=0):
         self.dev, self.dtype = dev, dtype
         self.n_chains, self.per_launch = n_chains, per_launch
         self.model, self._keep = op.model(dtype, dev)
@@ -82,7 +83,7 @@ class Workload:
         call("ipmc_potential", C.byref(self.model), adt, n_chains, self.u.data_ptr(), self.y.data_ptr(),
              self.ginv.data_ptr(), self.phi.data_ptr(), self.stream)
         s = _abi.IpmcSweep()
-        s.dtype, s.lanes_per_chain, s.chains_per_lane = adt, lanes, chains_per_lane
+        s.dtype, s.lanes_per_chain, s.chains_per_lane, s.spec_width = adt, lanes, chains_per_lane, spec_width
         s.n_chains, s.chain_offset = n_chains, chain_offset
         s.u, s.phi, s.accepts = self.u.data_ptr(), self.phi.data_ptr(), self.acc.data_ptr()
         s.y, s.gamma_inv, s.prior_sqrt = self.y.data_ptr(), self.ginv.data_ptr(), self.sq.data_ptr()
@@ -222,10 +223,14 @@ def launch_ranks(n):
 
 
 def auto_per_launch(chains_per_rank):
-    """pCN steps per launch: 1 when the rank's chains fill the GPU (65 536
-    lanes at 1 chain per lane group), more when they do not, so the sweep can
-    speculate over the steps of a launch (ipmc_plan_sweep)."""
-    return int(max(1, min(64, CHAINS_PER_GPU // max(1, chains_per_rank))))
+    """pCN steps per launch: 1 when the rank's chains fill a wave per SIMD on
+    their own (>= 16 384 chains, one launch per step), else 128, so that the
+    sweep speculates over the steps of a launch (ipmc_plan_sweep).  A launch
+    lasts as long as its slowest chain, so short speculative launches lose to
+    the chains that accept early: on this problem 8 192 chains ran 3.5 M steps/s
+    at 8 steps per launch, 14.8 M at 128, 10.9 M sequentially
+    (profiles/r3/bench_shards*.jsonl)."""
+    return 1 if chains_per_rank >= 16384 else 128
 
 
 def e2e_run(op, y, n_chains, chain_offset, dtype_np, dev, world, n_samples=20):
@@ -272,6 +277,7 @@ def main():
     ap.add_argument("--steps-per-launch", type=int, default=0, help="pCN steps per kernel launch (0 = auto)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--lanes", type=int, default=0)
+    ap.add_argument("--spec-width", type=int, default=0, help="speculative slots per chain (0 = auto, 1 = off)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -308,7 +314,8 @@ def main():
     per_rank = total_chains // world
     per_launch = args.steps_per_launch or auto_per_launch(per_rank)
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
-    w = Workload(op, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch)
+    w = Workload(op, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch,
+                 spec_width=args.spec_width)
     log(f"timing {args.steps} pCN steps ({args.dtype}, {per_rank} chains/GPU, {per_launch} steps/launch, "
         f"lanes={w.lanes}, spec_width={w.spec_width})")
     el, kern_ms = timed(w, args.steps, args.warmup, world)

@@ -177,14 +177,17 @@ static int l96_plan(const ipmc_model& m, const ipmc_sweep& s, int& lpc, int& cpl
         const int d = l96_dpp_lpc(m.dim, s.dtype, 1);
         if (d) l = d;
       }
-      // an ensemble that fills at least a quarter wave per SIMD on its own (a
-      // strong-scaled shard of the headline: 4 096 - 32 767 chains) speculates
-      // up to two waves per SIMD, in fp64 on the full ensemble's 2-lane layout:
-      // d=40, 8 192 chains x 8 steps per launch, 19.6 -> 20.2 M steps/s (fp64, 2
-      // lanes x 8 slots), 24.0 -> 25.4 M (fp32, 4 lanes x 4 slots); 16 384
-      // chains 19.6 -> 20.5 M / 24.1 -> 25.4 M (profiles/r3/shards.jsonl)
+      // an ensemble between a quarter and one wave per SIMD on the DPP layout
+      // (d=40: 4 096 - 16 383 chains, e.g. the 8 192-chain shard of a strong-
+      // scaled 65 536-chain run) speculates up to two waves per SIMD, in fp64 on
+      // the full ensemble's 2-lane layout.  The bench problem, 8 192 chains, 128
+      // steps per launch: 2 lanes x 8 slots 14.8 M steps/s, 8 x 2 13.7 M,
+      // sequential 10.9 M (profiles/r3/bench_shards_long.jsonl).  A launch lasts
+      // as long as its slowest chain, so at 16 384 chains, which fill a wave per
+      // SIMD sequentially, speculation lost on that problem (19.4 M sequential
+      // vs 17.2 - 18.9 M) and is not used.
       int64_t cap = 65536;
-      if (s.n_chains < 32768 && s.n_chains * (int64_t)l >= 16384) {
+      if (s.n_chains * (int64_t)l < 65536 && s.n_chains * (int64_t)l >= 16384) {
         cap = 131072;
         if (!s.lanes_per_chain && s.dtype == IPMC_F64 && m.dim % 2 == 0 && l96_has(m.dim, s.dtype, 2, 1)) l = 2;
       }

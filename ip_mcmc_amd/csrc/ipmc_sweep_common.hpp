@@ -188,6 +188,9 @@ struct SampleClock {
 // chain guesses "accept" while it accepts at least half of this launch's
 // steps; before its first round, `prior`.
 __device__ __forceinline__ bool spec_accept_mode(int64_t st, int64_t nacc, bool prior) {
+#ifdef IPMC_SPEC_REJECT_ONLY  // experiments (tools/build_variant.sh): the reject path only
+  return false;
+#endif
   return st == 0 ? prior : 2 * nacc >= st;
 }
 // The prior at a launch's first round: the chain's accept counter over the

@@ -249,6 +249,9 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     s3 = _sweep(n=32768)
     s3.n_steps = 2
     assert _plan(h, m, s3) == (2, 1, 1)  # 32 768 chains fill the GPU sequentially
+    s3 = _sweep(n=16384)
+    s3.n_steps = 8
+    assert _plan(h, m, s3) == (4, 1, 1)  # so do 16 384 on 4 lanes: no speculation
     s3 = _sweep(n=2048)
     s3.n_steps = 16
     assert _plan(h, m, s3) == (4, 1, 8)  # below a quarter wave per SIMD: one wave of slots

@@ -36,8 +36,9 @@ def test_auto_steps_per_launch():
     import bench
 
     assert bench.auto_per_launch(65536) == 1  # the full ensemble fills the GPU: one step per launch
-    assert bench.auto_per_launch(8192) == 8  # strong scaling over 8 GPUs: room to speculate
-    assert bench.auto_per_launch(1) == 64
+    assert bench.auto_per_launch(16384) == 1
+    assert bench.auto_per_launch(8192) == 128  # strong scaling over 8 GPUs: long speculative launches
+    assert bench.auto_per_launch(1) == 128
 
 
 def _committed_lines():

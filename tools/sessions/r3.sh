@@ -50,6 +50,26 @@ case "$1" in
       "shards:500:python tools/config_bench.py l96x65536 l96x32768@2 l96x16384@4 l96x8192@8 l96x4096@16 l96x2048@16 > gpurun_out/shards_rule.jsonl" \
       "bench8:300:python bench.py --chains 8192 --no-cpu > gpurun_out/bench_8192.json"
     ;;
+  g)  # strong-scaled shards on the bench's own problem: steps per launch 1 / 2 / 4 / 8 / 16
+    cmds=""
+    for c in 32768 16384 8192; do for l in 1 2 4 8 16; do
+      cmds="$cmds python bench.py --chains $c --steps-per-launch $l --steps 96 --warmup 16 --no-cpu --no-extra >> gpurun_out/bench_shards.jsonl &&"
+    done; done
+    tools/gpu_session.sh "shards:900:${cmds} true"
+    ;;
+  h)  # why speculative shards are slow on the bench problem: per-dispatch times, reject-only variant
+    V=ip_mcmc_amd/lib/variants
+    tools/gpu_session.sh \
+      "trace:300:rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace16k -o run -- python bench.py --chains 16384 --steps-per-launch 4 --steps 48 --warmup 8 --no-cpu --no-extra" \
+      "rejonly:300:IPMC_LIB_PATH=$V/rejonly/libipmc.so python bench.py --chains 16384 --steps-per-launch 4 --steps 96 --warmup 16 --no-cpu --no-extra > gpurun_out/bench_rejonly.jsonl && IPMC_LIB_PATH=$V/rejonly/libipmc.so python bench.py --chains 8192 --steps-per-launch 8 --steps 96 --warmup 16 --no-cpu --no-extra >> gpurun_out/bench_rejonly.jsonl"
+    ;;
+  i)  # shards on the bench problem: long launches, slots per chain
+    cmds=""
+    for c in 16384 8192; do for l in 32 128; do for sw in 0 2 4 1; do
+      cmds="$cmds python bench.py --chains $c --steps-per-launch $l --spec-width $sw --steps 256 --warmup 16 --no-cpu --no-extra >> gpurun_out/bench_shards_long.jsonl &&"
+    done; done; done
+    tools/gpu_session.sh "shards:1000:${cmds} true"
+    ;;
   c)  # the published line and its profiles from one box: bench, rocprofv3 --stats of the same
       # command, the three PMC passes (HBM bytes, clock, VALU issue) of the headline kernel
     tools/gpu_session.sh \
