@@ -224,13 +224,13 @@ def launch_ranks(n):
 
 def auto_per_launch(chains_per_rank):
     """pCN steps per launch: 1 when the rank's chains fill a wave per SIMD on
-    their own (>= 16 384 chains, one launch per step), else 128, so that the
+    their own (>= 16 384 chains, one launch per step), else 512, so that the
     sweep speculates over the steps of a launch (ipmc_plan_sweep).  A launch
     lasts as long as its slowest chain, so short speculative launches lose to
     the chains that accept early: on this problem 8 192 chains ran 3.5 M steps/s
-    at 8 steps per launch, 14.8 M at 128, 10.9 M sequentially
-    (profiles/r3/bench_shards*.jsonl)."""
-    return 1 if chains_per_rank >= 16384 else 128
+    at 8 steps per launch, 12.8 / 15.5 / 17.2 / 18.0 M at 64 / 128 / 256 / 512,
+    10.9 M sequentially (profiles/r3/bench_shards*.jsonl, bench_8192_long.jsonl)."""
+    return 1 if chains_per_rank >= 16384 else 512
 
 
 def e2e_run(op, y, n_chains, chain_offset, dtype_np, dev, world, n_samples=20):

@@ -37,8 +37,8 @@ def test_auto_steps_per_launch():
 
     assert bench.auto_per_launch(65536) == 1  # the full ensemble fills the GPU: one step per launch
     assert bench.auto_per_launch(16384) == 1
-    assert bench.auto_per_launch(8192) == 128  # strong scaling over 8 GPUs: long speculative launches
-    assert bench.auto_per_launch(1) == 128
+    assert bench.auto_per_launch(8192) == 512  # strong scaling over 8 GPUs: long speculative launches
+    assert bench.auto_per_launch(1) == 512
 
 
 def _committed_lines():
