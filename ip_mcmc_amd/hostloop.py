@@ -164,6 +164,10 @@ class _Misfit:
         if self.G is None:  # any potential object: its own value (constant included)
             return np.array([float(self.pot(v)) for v in V.astype(np.float64)], dtype=np.float64).astype(T)
         g = self.forward(V)
+        q = self.y_eff.shape[0] if self.diag else self.y_eff64.shape[0]
+        if g.ndim != 2 or g.shape[1] != q:
+            raise ValueError(f"the forward map returned {g.shape[1:] if g.ndim == 2 else g.shape} values per "
+                             f"parameter vector, the data have {q}")
         if self.diag:
             r = (self.y_eff[None, :] - g.astype(T)) * self.ginv[None, :]
             s = np.zeros(n, dtype=T)
@@ -232,7 +236,16 @@ def _schedule(plan, i0, n, T):
     return sched[:, 0].astype(T), sched[:, 1].astype(T)
 
 
-def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_samples, interval, rec, device):
+def _announce(verbose, done_steps, n_burn, interval, n_samples):
+    """sampler.py:24's per-sample print, before the block of sample i."""
+    if verbose and done_steps >= n_burn and (done_steps - n_burn) % interval == 0:
+        i = (done_steps - n_burn) // interval
+        if i < n_samples:
+            print(f"Sampling {i + 1}/{n_samples}")
+
+
+def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_samples, interval, rec, device,
+                   verbose=False):
     """Advance the chains (U [C, k] and Φ(U) [C], both dtype T, updated in
     place) by n_burn steps, then n_samples blocks of `interval` steps recording
     the state after each block (sampler.py:18-28).  Returns (accepts, calls per
@@ -252,6 +265,7 @@ def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_sam
                               device)
         betas, contrs = _schedule(plan, prop_i + done, nb, T)
         for s in range(nb):
+            _announce(verbose, done + s, n_burn, interval, n_samples)
             V = U + betas[s] * w[s] if plan.rw else contrs[s] * U + betas[s] * w[s]
             reach = np.ones(C_, dtype=bool)
             reached = []
@@ -343,7 +357,8 @@ def _counted(acc):
     return out
 
 
-def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_samples, interval, rec, device):
+def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_samples, interval, rec, device,
+                verbose=False):
     """The reference's _step (sampler.py:35-41) per chain with StepRNG draws.
     Returns per-chain (calls, accepts) of every CountedAccepter found."""
     C_, k = U.shape
@@ -359,6 +374,7 @@ def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_sampl
         nb = min(block, total - done)
         xi, r = DRAWS["raw"](seed, chain_offset, C_, step + done, nb, k, device)
         for s in range(nb):
+            _announce(verbose, done + s, n_burn, interval, n_samples)
             for c in range(C_):
                 before = [(ca.calls, ca.accepts) for ca in counted]
                 rng.set(xi[s, c], r[s, c])
@@ -440,7 +456,7 @@ def run(sampler, u_0, n_samples, burn_in, sample_interval, keep, sample_file, re
         else:
             phi = initial_phi(plan, U, device)
         acc_np, counts, total = run_structured(plan, U, phi, rng.seed, sampler.chain_offset, rng.step, prop_i,
-                                               n_burn, n_rec, eff_interval, rec, device)
+                                               n_burn, n_rec, eff_interval, rec, device, sampler.verbose)
         ci = 0
         inner = False
         for kind, obj in plan.layers:
@@ -457,7 +473,7 @@ def run(sampler, u_0, n_samples, burn_in, sample_interval, keep, sample_file, re
         counted = _counted(sampler.accepter)
         prev = [(ca.calls, ca.accepts) for ca in counted]
         counted, per, total = run_generic(sampler.proposer, sampler.accepter, U, rng.seed, sampler.chain_offset,
-                                          rng.step, n_burn, n_rec, eff_interval, rec, device)
+                                          rng.step, n_burn, n_rec, eff_interval, rec, device, sampler.verbose)
         acc_np = per[id(counted[0])][1] if counted else np.zeros(n_chains, dtype=np.int64)
         for ca, (c0, a0) in zip(counted, prev):
             # per-chain arrays for many chains, ints for one (the device path's convention)

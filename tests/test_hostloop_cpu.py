@@ -306,3 +306,20 @@ def test_float32_chains_round_like_the_kernels(odraws, orc):
     np.testing.assert_array_equal(last, Uo.astype(np.float64))
     np.testing.assert_array_equal(s.state.phi, phio)
     assert np.array_equal(s.accepter.accepts, acco) and acco.sum() > 0
+
+
+def test_verbose_prints_per_sample_and_shape_errors(odraws, golden, capsys):
+    """verbose=True prints sampler.py:24's 'Sampling i/n' and the acceptance
+    ratio (:30-31); a forward map returning the wrong number of values raises."""
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))),
+                    CountedAccepter(pCNAccepter(pot)), PhiloxRNG(seed), verbose=True)
+    s.run(np.zeros(4), n_samples=3, burn_in=5, sample_interval=2)
+    out = capsys.readouterr().out.splitlines()
+    assert out[:3] == ["Sampling 1/3", "Sampling 2/3", "Sampling 3/3"] and out[3].startswith("Acceptance ratio")
+    bad = EvolutionPotential(lambda u: np.array([1.0, 2.0]), golden["lin_y"], GaussianDistribution(0, gamma**2))
+    s = MCMCSampler(ConstSteppCNProposer(beta, GaussianDistribution(np.zeros(4), np.eye(4))), pCNAccepter(bad),
+                    PhiloxRNG(seed))
+    with pytest.raises(ValueError, match="forward map returned"):
+        s.run(np.zeros(4), n_samples=2, burn_in=0, sample_interval=1)
