@@ -56,6 +56,12 @@ def _case(case, rng):
         op = (Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=40) if case == "l63_hi"
               else LinearOperator(rng.normal(size=(3, 4))))
         return op, op(np.zeros(op.k)) + 0.2 * rng.normal(size=op.q), 50.0, 64, {}
+    if case == "burgers_hi":  # broad posterior: the Burgers sweep speculates along the accept path
+        op = BurgersOperator(N=32, dt_mode="cfl", T=0.3)
+        return op, op(np.zeros(3)) + 0.05 * rng.normal(size=5), 5.0, 16, {}
+    if case == "l96_hi":
+        op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=50)
+        return op, op(np.zeros(8)) + 0.1 * rng.normal(size=8), 10.0, 300, {}
     if case in ("ts", "ts_hi"):
         op = TwoScaleLorenz96Operator(4, 2, dt=0.005, n_steps=40)
         return op, op(np.zeros(3)) + 0.1 * rng.normal(size=op.q), (0.5 if case == "ts" else 50.0), 40, {}
@@ -73,7 +79,8 @@ def _case(case, rng):
 
 
 @pytest.mark.parametrize("case", ["linear1", "linear4096", "l96", "l96_var", "l96_seq", "l96_f32", "l63", "l63_f32",
-                                  "burgers", "ts", "l63_hi", "linear_hi", "ts_hi", "ts6", "ts6_hi"])
+                                  "burgers", "ts", "l63_hi", "linear_hi", "ts_hi", "ts6", "ts6_hi", "l96_hi",
+                                  "burgers_hi"])
 @pytest.mark.parametrize("keep", ["samples", "moments"])
 def test_pcn_run_equals_per_sample_launches(dev, case, keep):
     """In-launch samples (ipmc_sweep.sample_every, several samples per launch

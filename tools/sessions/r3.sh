@@ -70,6 +70,12 @@ case "$1" in
     done; done; done
     tools/gpu_session.sh "shards:1000:${cmds} true"
     ;;
+  v)  # validation of the tree as committed: the whole GPU suite (verbose), smoke, the default bench line
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -v" \
+      "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" \
+      "bench:400:python bench.py > gpurun_out/bench_line.json"
+    ;;
   c)  # the published line and its profiles from one box: bench, rocprofv3 --stats of the same
       # command, the three PMC passes (HBM bytes, clock, VALU issue) of the headline kernel
     tools/gpu_session.sh \
