@@ -80,6 +80,9 @@ def device_raw_draws(seed, chain_offset, n_chains, step0, n_steps, k, device=Non
 # the providers the loop uses (tests on a CPU-only machine substitute the
 # oracle's draws for these; the product path has no other source)
 DRAWS = {"w": device_draws, "raw": device_raw_draws}
+# run_structured's one-chain f64 loop on Python floats (tests switch it off to
+# compare it with the array loop)
+SINGLE_CHAIN_FLOATS = True
 
 
 class GenericComposition(Exception):
@@ -259,11 +262,65 @@ def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_sam
     block = max(1, min(total, DRAW_BLOCK_BYTES // max(1, C_ * k * U.itemsize)))
     done = 0
     post = 0  # post-burn-in steps done
+    # one f64 chain, a Python G and a diagonal noise (the reference's own use,
+    # e.g. config 1's script): the same operations on Python floats (IEEE
+    # doubles, as numpy's), without numpy's per-call overhead on 1-element arrays
+    single = (SINGLE_CHAIN_FLOATS and C_ == 1 and T is np.float64 and misfit.G is not None and misfit.diag
+              and not isinstance(misfit.G, ObservationOperator)
+              and (plan.reg_prior is None or plan.reg_prior.is_diagonal))
+    if single:
+        ul, ph = U[0].tolist(), float(phi[0])
+        yl, gil = misfit.y_eff.tolist(), misfit.ginv.tolist()
+        rsl = None if plan.reg_prior is None else plan.reg_prior.sqrt_diagonal.tolist()
     while done < total:
         nb = min(block, total - done)
         w, log_r = DRAWS["w"](seed, chain_offset, C_, step + done, nb, k, T, plan.prior_sqrt, plan.prior_chol,
                               device)
         betas, contrs = _schedule(plan, prop_i + done, nb, T)
+        if single:
+            wl, lrl, bl, cl = w[:, 0, :].tolist(), log_r[:, 0].tolist(), betas.tolist(), contrs.tolist()
+            for s in range(nb):
+                _announce(verbose, done + s, n_burn, interval, n_samples)
+                b, ws = bl[s], wl[s]
+                if plan.rw:
+                    v = [ui + b * wi for ui, wi in zip(ul, ws)]
+                else:
+                    c = cl[s]
+                    v = [c * ui + b * wi for ui, wi in zip(ul, ws)]
+                reach, ci = True, 0
+                for kind, obj in plan.layers:
+                    if kind == "count":
+                        counts[ci][0] += reach
+                        ci += 1
+                    elif reach:
+                        reach = bool(obj(np.array(v)))
+                if reach:
+                    g = np.atleast_1d(np.asarray(misfit.G(np.array(v)), dtype=np.float64)).reshape(-1).tolist()
+                    if len(g) != len(yl):
+                        raise ValueError(f"the forward map returned {len(g)} values per parameter vector, the data "
+                                         f"have {len(yl)}")
+                    sm = 0.0
+                    for yi, gv, gi in zip(yl, g, gil):  # component order, no FMA
+                        r = (yi - gv) * gi
+                        sm = sm + r * r
+                    phv = 0.5 * sm
+                    if rsl is not None:
+                        s2 = 0.0
+                        for cj, vj in zip(rsl, v):
+                            t = cj * vj
+                            s2 = s2 + t * t
+                        phv = phv + 0.5 * s2
+                    if (ph - phv) > lrl[s]:
+                        ul, ph = v, phv
+                        acc_total[0] += 1
+                if done + s >= n_burn:
+                    if rec.sum_u is not None:
+                        rec.accumulate(np.array([ul]))
+                    post += 1
+                    if post % interval == 0:
+                        rec.record(post // interval - 1, np.array([ul]))
+            done += nb
+            continue
         for s in range(nb):
             _announce(verbose, done + s, n_burn, interval, n_samples)
             V = U + betas[s] * w[s] if plan.rw else contrs[s] * U + betas[s] * w[s]
@@ -298,6 +355,9 @@ def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_sam
                 if post % interval == 0:
                     rec.record(post // interval - 1, U)
         done += nb
+    if single:
+        U[0] = ul
+        phi[0] = ph
     return acc_total, counts, total
 
 

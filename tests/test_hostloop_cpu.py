@@ -323,3 +323,33 @@ def test_verbose_prints_per_sample_and_shape_errors(odraws, golden, capsys):
                     PhiloxRNG(seed))
     with pytest.raises(ValueError, match="forward map returned"):
         s.run(np.zeros(4), n_samples=2, burn_in=0, sample_interval=1)
+
+
+@pytest.mark.parametrize("keep", ["samples", "moments", "last"])
+def test_single_chain_float_loop_equals_array_loop(orc, odraws, golden, monkeypatch, keep):
+    """One f64 chain runs the host step on Python floats; it equals the array
+    loop bit for bit -- RW with the prior regularizer, a predicate, two counted
+    layers and each recording mode (the pCN case is pinned to the fixture by
+    test_python_G_single_chains_match_reference_fixture)."""
+    meta = golden["bch_meta"]
+    gamma, sigma_p, seed = meta[1], meta[2], int(meta[4])
+    d_s, d_e, l = meta[8], meta[9], meta[10]
+    A = np.random.default_rng(5).normal(size=(5, 3))
+    prior = GaussianDistribution(np.zeros(3), np.diag([sigma_p**2, 0.5 * sigma_p**2, 2 * sigma_p**2]))
+    pot = EvolutionPotential(lambda u: A @ u, A @ np.array([0.1, -0.2, 0.3]) + 0.05,
+                             GaussianDistribution(np.zeros(5), gamma**2 * np.eye(5)))
+    runs = []
+    for fast in (True, False):
+        monkeypatch.setattr(hostloop, "SINGLE_CHAIN_FLOATS", fast)
+        inner = CountedAccepter(StandardRWAccepter(pot, prior))
+        outer = CountedAccepter(ConstrainAccepter(inner, lambda u: abs(u[2]) < 0.4))
+        s = MCMCSampler(VarStepStandardRWProposer(PWLinear(d_s, d_e, l), prior), outer, PhiloxRNG(seed),
+                        chain_offset=3)
+        out = s.run(np.zeros(3), n_samples=40, burn_in=17, sample_interval=3, keep=keep)
+        runs.append((out, inner.calls, inner.accepts, outer.calls, outer.accepts, s.state.u, s.state.phi))
+    for a, b in zip(*runs):
+        if isinstance(a, dict):
+            assert a.keys() == b.keys() and all(np.array_equal(a[key], b[key]) for key in a)
+        else:
+            assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert 0 < runs[0][2] < runs[0][1] < runs[0][3]
