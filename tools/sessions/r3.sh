@@ -17,6 +17,24 @@ case "$1" in
       "cfg2:300:python tools/config_bench.py cfg2@128 cfg2g1@128 cfg2 > gpurun_out/cfg2.jsonl" \
       "stuart:400:python examples/stuart_reference.py > gpurun_out/stuart_reference.jsonl"
     ;;
+  k)  # L96 FMA arith with the forcing folded into the stage bases (18 instead of 20 FP64 ops per component-step)
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "bench:400:python bench.py > gpurun_out/bench_line_fold.json" \
+      "configs:500:python tools/config_bench.py cfg5 l96x1@256 l96x64@256 l96x1024@64 l96x8192@8 > gpurun_out/configs_fold.jsonl" \
+      "arith:600:python tools/arith_agreement.py 100 0.2 0.05 0.02 > gpurun_out/arith_agreement_fold.jsonl"
+    ;;
+  m)  # A/B: the folded-forcing L96 kernels against the previous ones (variants/oldl96), bench + SQ pass each
+    O=ip_mcmc_amd/lib/variants/oldl96/libipmc.so
+    BB="python bench.py --steps 100 --warmup 5 --no-cpu --no-extra"
+    tools/gpu_session.sh \
+      "ab1:300:$BB > gpurun_out/ab_new.jsonl && IPMC_LIB_PATH=$O $BB > gpurun_out/ab_old.jsonl" \
+      "ab2:300:$BB >> gpurun_out/ab_new.jsonl && IPMC_LIB_PATH=$O $BB >> gpurun_out/ab_old.jsonl" \
+      "f32:300:$BB --dtype f32 >> gpurun_out/ab_new.jsonl && IPMC_LIB_PATH=$O $BB --dtype f32 >> gpurun_out/ab_old.jsonl" \
+      "lanes4:300:$BB --dtype f32 --lanes 4 >> gpurun_out/ab_new.jsonl && IPMC_LIB_PATH=$O $BB --dtype f32 --lanes 4 >> gpurun_out/ab_old.jsonl && $BB --lanes 4 >> gpurun_out/ab_new.jsonl && IPMC_LIB_PATH=$O $BB --lanes 4 >> gpurun_out/ab_old.jsonl" \
+      "sq_new:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_fold_new -o run -- python bench.py --steps 10 --warmup 2 --no-cpu --no-extra" \
+      "sq_old:200:IPMC_LIB_PATH=$O timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_fold_old -o run -- python bench.py --steps 10 --warmup 2 --no-cpu --no-extra"
+    ;;
   b)  # accept-path speculation (small models) and the K=6 two-scale layouts (SPL 3 DPP pairs / 1 / 6)
     V=ip_mcmc_amd/lib/variants
     tools/gpu_session.sh \
