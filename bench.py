@@ -227,9 +227,11 @@ def auto_per_launch(chains_per_rank):
     their own (>= 16 384 chains, one launch per step), else 512, so that the
     sweep speculates over the steps of a launch (ipmc_plan_sweep).  A launch
     lasts as long as its slowest chain, so short speculative launches lose to
-    the chains that accept early: on this problem 8 192 chains ran 3.5 M steps/s
-    at 8 steps per launch, 12.8 / 15.5 / 17.2 / 18.0 M at 64 / 128 / 256 / 512,
-    10.9 M sequentially (profiles/r3/bench_shards*.jsonl, bench_8192_long.jsonl)."""
+    the chains that accept early; the sweep therefore speculates only up to one
+    wave per SIMD (8 192 chains: 4 lanes x 2 slots), which ran this problem at
+    11.4 / 18.0 / 18.8 M steps/s with 20 / 200 / 512 steps per launch, against
+    5.9 / 15.6 / 18.9 M for 2 lanes x 8 slots and 10.4 / 10.8 M sequentially
+    (profiles/r3/bench_8192_short.jsonl, bench_shards_l4.jsonl)."""
     return 1 if chains_per_rank >= 16384 else 512
 
 

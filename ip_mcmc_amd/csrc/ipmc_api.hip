@@ -177,20 +177,15 @@ static int l96_plan(const ipmc_model& m, const ipmc_sweep& s, int& lpc, int& cpl
         const int d = l96_dpp_lpc(m.dim, s.dtype, 1);
         if (d) l = d;
       }
-      // an ensemble between a quarter and one wave per SIMD on the DPP layout
-      // (d=40: 4 096 - 16 383 chains, e.g. the 8 192-chain shard of a strong-
-      // scaled 65 536-chain run) speculates up to two waves per SIMD, in fp64 on
-      // the full ensemble's 2-lane layout.  The bench problem, 8 192 chains, 128
-      // steps per launch: 2 lanes x 8 slots 14.8 M steps/s, 8 x 2 13.7 M,
-      // sequential 10.9 M (profiles/r3/bench_shards_long.jsonl).  A launch lasts
-      // as long as its slowest chain, so at 16 384 chains, which fill a wave per
-      // SIMD sequentially, speculation lost on that problem (19.4 M sequential
-      // vs 17.2 - 18.9 M) and is not used.
-      int64_t cap = 65536;
-      if (s.n_chains * (int64_t)l < 65536 && s.n_chains * (int64_t)l >= 16384) {
-        cap = 131072;
-        if (!s.lanes_per_chain && s.dtype == IPMC_F64 && m.dim % 2 == 0 && l96_has(m.dim, s.dtype, 2, 1)) l = 2;
-      }
+      // slots fill at most one wave per SIMD.  A launch lasts as long as its
+      // slowest chain, and on the bench problem (chains burning in from u = 0)
+      // wider speculation loses most where launches are short: 8 192 chains,
+      // 20 / 200 / 512 steps per launch, 4 lanes x 2 slots (this rule) 11.4 /
+      // 18.0 / 18.8 M steps/s, 2 lanes x 8 slots (two waves per SIMD, round 3's
+      // earlier rule) 5.9 / 15.6 / 18.9 M, sequential on 8 lanes 10.4 / 10.8 M
+      // (profiles/r3/bench_8192_short.jsonl, bench_shards_l4.jsonl); on
+      // config_bench's problem, which accepts almost nothing, 19.6 vs 20.2 M.
+      const int64_t cap = 65536;
       int w = 1;
       while (w * 2 * l <= 64 && s.n_chains * (int64_t)l * w * 2 <= cap) w *= 2;
       // a whole block of slots per chain (4 waves on the CU's 4 SIMDs) while

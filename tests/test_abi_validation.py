@@ -242,9 +242,9 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 8192) == 108  # one step: LDS halos fill the GPU
     assert _plan(h, m, s) == (8, 1, 1)
     s.n_steps = 16
-    assert _plan(h, m, s) == (2, 1, 8)  # multi-step: the 2-lane layout, 8 slots (two waves per SIMD)
+    assert _plan(h, m, s) == (4, 1, 2)  # multi-step: the DPP layout, 2 slots (one wave per SIMD)
     s.dtype = _abi.F32
-    assert _plan(h, m, s) == (4, 1, 4)  # fp32: 4 lanes x 4 slots
+    assert _plan(h, m, s) == (4, 1, 2)  # fp32 the same
     s.dtype = _abi.F64
     s3 = _sweep(n=32768)
     s3.n_steps = 2
@@ -254,7 +254,7 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     assert _plan(h, m, s3) == (4, 1, 1)  # so do 16 384 on 4 lanes: no speculation
     s3 = _sweep(n=2048)
     s3.n_steps = 16
-    assert _plan(h, m, s3) == (4, 1, 8)  # below a quarter wave per SIMD: one wave of slots
+    assert _plan(h, m, s3) == (4, 1, 8)  # slots up to one wave per SIMD
     s = _sweep(n=1)
     s.n_steps = 16
     assert _plan(h, m, s) == (4, 1, 64)  # one chain: its slots span a whole block

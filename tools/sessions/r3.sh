@@ -35,6 +35,22 @@ case "$1" in
       "sq_new:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_fold_new -o run -- python bench.py --steps 10 --warmup 2 --no-cpu --no-extra" \
       "sq_old:200:IPMC_LIB_PATH=$O timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_fold_old -o run -- python bench.py --steps 10 --warmup 2 --no-cpu --no-extra"
     ;;
+  n)  # strong-scaled shards on the bench problem: 4 lanes per chain with 1 / 2 / 4 slots, 512-step launches
+    cmds=""
+    for c in 8192 16384; do for lw in "2 0" "4 1" "4 2" "4 4" "2 2" "2 4"; do set -- $lw
+      cmds="$cmds python bench.py --chains $c --lanes $1 --spec-width $2 --steps-per-launch 512 --steps 1024 --warmup 512 --no-cpu --no-extra >> gpurun_out/bench_shards_l4.jsonl &&"
+    done; done
+    tools/gpu_session.sh "shards:900:${cmds} true"
+    ;;
+  o)  # the 8-GPU strong-scaled shard (8 192 chains) at short timed regions: K = 20 / 200 steps, layouts
+    cmds=""
+    for K in "20 5" "200 10"; do set -- $K; k=$1; w=$2
+      for lw in "2 0" "2 4" "4 2" "4 4" "8 1" "4 1"; do set -- $lw
+        cmds="$cmds python bench.py --chains 8192 --lanes $1 --spec-width $2 --steps $k --warmup $w --no-cpu --no-extra >> gpurun_out/bench_8192_short.jsonl &&"
+      done
+    done
+    tools/gpu_session.sh "short:900:${cmds} true"
+    ;;
   b)  # accept-path speculation (small models) and the K=6 two-scale layouts (SPL 3 DPP pairs / 1 / 6)
     V=ip_mcmc_amd/lib/variants
     tools/gpu_session.sh \
