@@ -227,11 +227,11 @@ def auto_per_launch(chains_per_rank):
     their own (>= 16 384 chains, one launch per step), else 512, so that the
     sweep speculates over the steps of a launch (ipmc_plan_sweep).  A launch
     lasts as long as its slowest chain, so short speculative launches lose to
-    the chains that accept early; the sweep therefore speculates only up to one
-    wave per SIMD (8 192 chains: 4 lanes x 2 slots), which ran this problem at
-    11.4 / 18.0 / 18.8 M steps/s with 20 / 200 / 512 steps per launch, against
-    5.9 / 15.6 / 18.9 M for 2 lanes x 8 slots and 10.4 / 10.8 M sequentially
-    (profiles/r3/bench_8192_short.jsonl, bench_shards_l4.jsonl)."""
+    the chains that accept early: 8 192 chains run sequentially on 8
+    interleaved lanes below 256 steps per launch and speculate on 4 lanes x 2
+    slots from there (ipmc_plan_sweep): 14.4 / 16.6 / 17.8 M steps/s on this
+    problem at 20 / 200 / 1 024 timed steps, where round 3's first rule (2
+    lanes x 8 slots) ran 5.9 / 15.6 / 18.9 M (profiles/r3/bench_8192_*.jsonl)."""
     return 1 if chains_per_rank >= 16384 else 512
 
 
@@ -314,7 +314,8 @@ def main():
     if total_chains % world:
         raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
     per_rank = total_chains // world
-    per_launch = args.steps_per_launch or auto_per_launch(per_rank)
+    # (a launch never exceeds the timed steps: the plan reported is the one timed)
+    per_launch = min(args.steps_per_launch or auto_per_launch(per_rank), max(1, args.steps))
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     w = Workload(op, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch,
                  spec_width=args.spec_width)

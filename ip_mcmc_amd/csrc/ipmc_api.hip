@@ -86,14 +86,18 @@ static bool l96_has(int D, int dtype, int lpc, int cpl) {
 
 // Layout choice for Lorenz-96 (lanes per chain LPC, chains per lane group CPL),
 // from the layout scans of profiles/r1/lanes_scan_*.txt and lanes_layout_rule.txt:
-//  1. the fewest lanes per chain whose halos go by DPP (LPC 1, 2, 4, 16) that
+//  1. the fewest lanes per chain whose halos go by DPP (LPC 1, 2, 4, 8, 16) that
 //     still gives every SIMD one wave (kWaveLanes lanes), packed fp32 (CPL 2)
 //     first; more lanes only add halo work, fewer leave SIMDs idle.  With more
 //     than 20 components per lane (the in-place RK4 state, l96_stage, no
 //     longer fits 256 VGPRs) the next layout (LPC 2 -> 4, <= 4 waves).
 //     d=40, 65 536 chains, LPC 2 vs 4 on the same box: packed fp32 1.75 vs
 //     1.85 ms, fp64 3.32 vs 3.37 ms (profiles/r2/lanes_scan_d40_r2k.txt);
-//  2. else any compiled layout reaching one wave (LPC 8: halos through LDS);
+//     (LPC 8 since round 3: two chains interleaved per row of 16 lanes, one
+//     DPP row rotation per halo dword, group_vlane in ipmc_device.hpp; d=40,
+//     8 192 chains: 14.7 / 17.1 M steps/s at 20 / 200 steps per launch, 10.4 /
+//     10.8 M with ds_bpermute halos, profiles/r3/bench_8192_l8dpp.jsonl);
+//  2. else any compiled layout reaching one wave;
 //  3. else (an ensemble below one wave per SIMD, where the speculative sweep
 //     fills lanes with slots) the most DPP lanes per chain that keep >= 4
 //     components per lane: a chain's RK4 step is then a latency chain, and
@@ -112,7 +116,7 @@ static int l96_dpp_lpc(int D, int dtype, int cpl) {
 
 static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   constexpr int64_t kWaveLanes = 65536;  // 256 CUs x 4 SIMDs x 64 lanes
-  static const int dpp[4] = {1, 2, 4, 16};
+  static const int dpp[5] = {1, 2, 4, 8, 16};
   static const int all[5] = {1, 2, 4, 8, 16};
   const int ncpl = dtype == IPMC_F32 ? 2 : 1;
   const int cpls[2] = {ncpl, 1};
@@ -120,7 +124,7 @@ static void l96_layout(int D, int dtype, int64_t n_chains, int& lpc, int& cpl) {
   for (int ci = 0; ci < ncpl; ++ci) {
     const int c = cpls[ci];
     const int64_t groups = (n_chains + c - 1) / c;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
       int l = dpp[i];
       if (!ok(l, c) || groups * l < kWaveLanes) continue;
       // beyond 20 components per lane the in-place RK4 state (5 arrays) no
@@ -168,10 +172,17 @@ static int l96_plan(const ipmc_model& m, const ipmc_sweep& s, int& lpc, int& cpl
     return fail(IPMC_ERR_UNSUPPORTED, "spec_width must be a power of two <= 256");
   if (spec == 0) {
     spec = 1;
-    if (s.n_steps > 1 && s.chains_per_lane != 2) {
-      // speculative slots run on the DPP layout (an LDS-halo layout picked to
-      // fill the GPU with sequential chains is slower than DPP slots: d=40,
-      // 8 192 chains, profiles/r1/small_ensembles.jsonl)
+    // an auto layout that already fills a wave per SIMD (since LPC 8 halos go
+    // by DPP: 8 192 chains of d=40 on 8 lanes) runs sequentially unless the
+    // launch is long: a launch lasts as long as its slowest chain, which costs
+    // speculation most on short launches (bench problem, 8 192 chains, 20 /
+    // 200 / 512 steps per launch: 8 lanes sequential 14.7 / 17.1 / -- M
+    // steps/s, 4 lanes x 2 slots 10.7 / 17.7 / 18.8 M)
+    const int64_t groups = (s.n_chains + cpl - 1) / cpl;
+    const bool fills = !s.lanes_per_chain && groups * lpc >= 65536;
+    if (s.n_steps > 1 && s.chains_per_lane != 2 && (!fills || s.n_steps >= 256)) {
+      // speculative slots run on the quad / row DPP layout (l96_dpp_lpc: the
+      // speculative kernel's LPC 8 halos take two DPP moves and a select)
       int l = lpc;
       if (!s.lanes_per_chain) {
         const int d = l96_dpp_lpc(m.dim, s.dtype, 1);

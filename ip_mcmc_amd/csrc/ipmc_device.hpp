@@ -221,30 +221,63 @@ constexpr int kRowRor15 = 0x12F;
 // (DPP movs take VALU issue slots -- 24 of the 224 instructions of a d=40
 // RK4 step at LPC 4 -- but moving these halos to ds_bpermute measured 10 %
 // slower: profiles/r1/halo_dpp_vs_lds.txt.)
-template <int LPC, typename T>
+// Half rows (LPC 8) have no rotation of their own: lane i reads lane i-1
+// (row_shr:1) except at the half's first lane, which reads the half's last
+// (row_shl:7), and the select is one v_cndmask per dword -- three VALU ops
+// instead of a ds_bpermute round trip, whose latency one wave per SIMD (the
+// 8 192-chain ensemble on 8 lanes) cannot hide.
+constexpr int kRowShl1 = 0x101;
+constexpr int kRowShl7 = 0x107;
+constexpr int kRowShr1 = 0x111;
+constexpr int kRowShr7 = 0x117;
+constexpr int kRowRor2 = 0x122;
+constexpr int kRowRor14 = 0x12E;
+
+// Interleaved groups of 8 (IL; the sequential Lorenz-96 kernels): each row of
+// 16 lanes holds two chains, one on its even lanes and one on its odd lanes,
+// so a DPP row rotation by 2 is a halo move for both -- one VALU op per dword,
+// as for LPC 16.  The lane's place in its group follows from the virtual
+// thread index group_vlane(t): chain = vt / 8, sub = vt % 8.
+template <int LPC, bool IL>
+__device__ __forceinline__ int group_vlane(int t) {
+  if constexpr (IL && LPC == 8) return (t & ~15) | ((t & 1) << 3) | ((t >> 1) & 7);
+  else return t;
+}
+
+template <int LPC, bool IL = false, typename T>
 __device__ __forceinline__ T group_prev(T v, int lane) {
   if constexpr (LPC == 1) return v;
   else if constexpr (LPC == 2) return dpp<qperm(1, 0, 3, 2)>(v);
   else if constexpr (LPC == 4) return dpp<qperm(3, 0, 1, 2)>(v);
-  else if constexpr (LPC == 16) return dpp<kRowRor1>(v);
+  else if constexpr (LPC == 8 && IL) return dpp<kRowRor2>(v);
+  else if constexpr (LPC == 8) {
+    const T a = dpp<kRowShr1>(v), b = dpp<kRowShl7>(v);
+    return (lane & 7) == 0 ? b : a;
+  } else if constexpr (LPC == 16) return dpp<kRowRor1>(v);
   else return shfl(v, (lane & ~(LPC - 1)) | ((lane - 1) & (LPC - 1)));
 }
-template <int LPC, typename T>
+template <int LPC, bool IL = false, typename T>
 __device__ __forceinline__ T group_next(T v, int lane) {
   if constexpr (LPC == 1) return v;
   else if constexpr (LPC == 2) return dpp<qperm(1, 0, 3, 2)>(v);
   else if constexpr (LPC == 4) return dpp<qperm(1, 2, 3, 0)>(v);
-  else if constexpr (LPC == 16) return dpp<kRowRor15>(v);
+  else if constexpr (LPC == 8 && IL) return dpp<kRowRor14>(v);
+  else if constexpr (LPC == 8) {
+    const T a = dpp<kRowShl1>(v), b = dpp<kRowShr7>(v);
+    return (lane & 7) == 7 ? b : a;
+  } else if constexpr (LPC == 16) return dpp<kRowRor15>(v);
   else return shfl(v, (lane & ~(LPC - 1)) | ((lane + 1) & (LPC - 1)));
 }
 // Value of `v` held by lane `s` of this chain's group.
-template <int LPC, int S, typename T>
+template <int LPC, int S, bool IL = false, typename T>
 __device__ __forceinline__ T group_bcast(T v, int lane) {
   if constexpr (LPC == 1) return v;
   else if constexpr (LPC <= 4) {
     // within a quad: group base lane b = (i & ~(LPC-1)); source = b + S
     if constexpr (LPC == 2) return dpp<qperm(S, S, 2 + S, 2 + S)>(v);
     else return dpp<qperm(S, S, S, S)>(v);
+  } else if constexpr (LPC == 8 && IL) {
+    return shfl(v, (lane & ~15) | (S << 1) | (lane & 1));
   } else {
     return shfl(v, (lane & ~(LPC - 1)) | S);
   }
@@ -258,10 +291,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // All lanes of the group hold `ok`: true iff every lane's ok is true.
-template <int LPC>
+template <int LPC, bool IL = false>
 __device__ __forceinline__ bool group_all(bool ok, int lane) {
   if constexpr (LPC == 1) return ok;
   const unsigned long long m = __ballot(ok);
+  if constexpr (LPC == 8 && IL) {  // this chain's lanes: every other lane of the row
+    const unsigned long long g = (m >> (lane & ~15)) & (0x5555ull << (lane & 1));
+    return g == (0x5555ull << (lane & 1));
+  }
   const unsigned long long g = (m >> (lane & ~(LPC - 1))) & ((1ull << LPC) - 1);
   return g == ((1ull << LPC) - 1);
 }

@@ -6,37 +6,15 @@
 // post-step states.  The state of one chain lives in VGPRs of a group of LPC
 // lanes (M = D/LPC components per lane); the cyclic neighbours X_{k-2},
 // X_{k-1}, X_{k+1} that cross a lane boundary come from the neighbour lanes by
-// DPP (LPC 2/4) or ds_bpermute (LPC 8/16).  Nothing touches HBM inside the RK
+// DPP: quad permutations (LPC 2/4), row rotations (LPC 16; LPC 8 with two
+// chains interleaved per row in the sequential kernels, shifts and a select in
+// the speculative one).  Nothing touches HBM inside the RK
 // loop: the kernel is VALU-bound.
 #pragma once
 
 #include "ipmc_sweep_common.hpp"
 
 namespace ipmc {
-
-// dX/dt for the lane's M components.
-//   FM:  out_k = fma(X_{k+1} - X_{k-2}, X_{k-1}, F_k - X_k)          3 VALU ops
-//   REF: out_k = ((-X_k) - (X_{k-1} X_{k-2} - X_{k-1} X_{k+1})) + F_k  lorenz.py:77-81
-template <typename T, int M, int LPC, bool FM>
-__device__ __forceinline__ void l96_rhs(const T (&s)[M], const T (&F)[M], T (&o)[M], int lane) {
-  static_assert(M >= 2, "Lorenz-96 needs at least 2 components per lane");
-  const T sl1 = group_prev<LPC>(s[M - 1], lane);
-  const T sl2 = group_prev<LPC>(s[M - 2], lane);
-  const T sr1 = group_next<LPC>(s[0], lane);
-#pragma unroll
-  for (int j = 0; j < M; ++j) {
-    const T xm1 = (j >= 1) ? s[j - 1] : sl1;
-    const T xm2 = (j >= 2) ? s[j - 2] : ((j == 1) ? sl1 : sl2);
-    const T xp1 = (j < M - 1) ? s[j + 1] : sr1;
-    if constexpr (FM) {
-      o[j] = madd<true>(xp1 - xm2, xm1, F[j] - s[j]);
-    } else {
-      T t = -s[j];
-      t = t - (xm1 * xm2 - xm1 * xp1);
-      o[j] = t + F[j];
-    }
-  }
-}
 
 // One classical RK4 stage with every rate consumed as soon as it is computed
 // (no array of rates; cf. ts_stage in ipmc_l96ts.hip):
@@ -47,13 +25,13 @@ __device__ __forceinline__ void l96_rhs(const T (&s)[M], const T (&F)[M], T (&o)
 // bits do not change.  The stage input's halos are fetched before anything is
 // written, and the old X_{j-1}, X_{j-2} ride along in p1, p2, so `in` may alias
 // `xs`: one array of M values fewer live in the RK loop.
-template <typename V, int M, int LPC, bool FM, int STAGE>
+template <typename V, int M, int LPC, bool FM, int STAGE, bool IL>
 __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (&acc)[M], V (&ob)[M],
                                           const V (&F)[M], V c, V two, int lane) {
   static_assert(M >= 2, "Lorenz-96 needs at least 2 components per lane");
-  const V sr1 = group_next<LPC>(in[0], lane);
-  V p2 = group_prev<LPC>(in[M - 2], lane);
-  V p1 = group_prev<LPC>(in[M - 1], lane);
+  const V sr1 = group_next<LPC, IL>(in[0], lane);
+  V p2 = group_prev<LPC, IL>(in[M - 2], lane);
+  V p1 = group_prev<LPC, IL>(in[M - 1], lane);
 #pragma unroll
   for (int j = 0; j < M; ++j) {
     const V cur = in[j];
@@ -84,8 +62,9 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
 
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
 // V is the per-lane storage type (float, double, or f32x2 = two fp32 chains),
-// S the scalar type of the problem constants.
-template <typename V, int M, int LPC, bool FM, typename S>
+// S the scalar type of the problem constants, IL: interleaved groups of 8
+// (group_vlane, ipmc_device.hpp).
+template <typename V, int M, int LPC, bool FM, bool IL = false, typename S>
 __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict__ x0, V h, int nsteps, int lane,
                                             V (&g)[M]) {
   using P = Splat<V>;
@@ -100,10 +79,10 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
   }
   for (int n = 0; n < nsteps; ++n) {
     V acc[M], xs[M];
-    l96_stage<V, M, LPC, FM, 1>(x, xs, x, acc, ob, F, h2, two, lane);
-    l96_stage<V, M, LPC, FM, 2>(xs, xs, x, acc, ob, F, h2, two, lane);
-    l96_stage<V, M, LPC, FM, 3>(xs, xs, x, acc, ob, F, h, two, lane);
-    l96_stage<V, M, LPC, FM, 4>(xs, xs, x, acc, ob, F, h6, two, lane);
+    l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);
+    l96_stage<V, M, LPC, FM, 2, IL>(xs, xs, x, acc, ob, F, h2, two, lane);
+    l96_stage<V, M, LPC, FM, 3, IL>(xs, xs, x, acc, ob, F, h, two, lane);
+    l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
   }
   const V nn = P::of((S)nsteps);
 #pragma unroll
@@ -120,7 +99,7 @@ constexpr int l96_stage_len() {
   return LPC >= 8 ? M * kL96Block : 1;
 }
 
-template <typename V, int M, int LPC, bool FM, typename S>
+template <typename V, int M, int LPC, bool FM, bool IL = false, typename S>
 __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict__ th0, const S* __restrict__ x0,
                                            const S* __restrict__ y, const S* __restrict__ ginv, V h, int nsteps,
                                            int lane, V* stage) {
@@ -128,11 +107,11 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
   V F[M], g[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) F[j] = P::of(th0[j]) + v[j];
-  l96_forward<V, M, LPC, FM>(F, x0, h, nsteps, lane, g);
+  l96_forward<V, M, LPC, FM, IL>(F, x0, h, nsteps, lane, g);
   V r[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) r[j] = (P::of(y[j]) - g[j]) * P::of(ginv[j]);
-  return P::of((S)0.5) * group_sumsq<V, M, LPC, FM, kL96Block>(r, lane, stage, P::of((S)0));
+  return P::of((S)0.5) * group_sumsq<V, M, LPC, FM, kL96Block, IL>(r, lane, stage, P::of((S)0));
 }
 
 // Occupancy target (waves per SIMD) the register allocator is held to: the
@@ -176,10 +155,11 @@ constexpr int l96_pk_waves_per_simd() {
 template <typename T, int D, int LPC, bool FM>
 __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void l96_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
   constexpr int M = D / LPC;
+  constexpr bool IL = (LPC == 8);  // interleaved groups of 8 (group_vlane)
   __shared__ T vpark[M][kL96Block];  // proposal parked in LDS while G runs
   __shared__ T stage[l96_stage_len<M, LPC>()];
   const int lane = threadIdx.x & 63;
-  const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * kL96Block + group_vlane<LPC, IL>(threadIdx.x);
   const int64_t chain = tid / LPC;
   const int sub = (int)(tid % LPC);
   if (chain >= s.n_chains) return;  // whole lane groups leave together
@@ -207,14 +187,14 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
     T v[M];
     pcn_propose<T, M>(u, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, cl, v, rw,
                       (const T*)s.prior_chol, D);
-    if (box_valid<T, M, LPC>(s, c0, v, lane)) {
+    if (box_valid<T, M, LPC, IL>(s, c0, v, lane)) {
       ++ncalls;
       const T reg = s.reg_scale
-                        ? regularizer<T, M, LPC, FM, T, kL96Block>((const T*)s.reg_scale + cl, v, lane, stage)
+                        ? regularizer<T, M, LPC, FM, T, kL96Block, IL>((const T*)s.reg_scale + cl, v, lane, stage)
                         : (T)0;
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x] = v[j];
-      T phv = l96_potential<T, M, LPC, FM>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
+      T phv = l96_potential<T, M, LPC, FM, IL>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
                                            (const T*)s.gamma_inv + cl, h, m.n_steps, lane, stage);
       if (s.reg_scale) phv = phv + reg;  // I(v) = Φ(v) + regularizer (accepter.py:106)
       // memory clobber: re-read v from LDS instead of keeping it live in VGPRs across G
@@ -456,10 +436,11 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     const ipmc_model m, const ipmc_sweep s) {
   constexpr int M = D / LPC;
   using V = f32x2;
+  constexpr bool IL = (LPC == 8);  // interleaved groups of 8 (group_vlane)
   __shared__ V vpark[M][kL96Block];
   __shared__ V stage[l96_stage_len<M, LPC>()];
   const int lane = threadIdx.x & 63;
-  const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * kL96Block + group_vlane<LPC, IL>(threadIdx.x);
   const int64_t pair = tid / LPC;
   const int sub = (int)(tid % LPC);
   const int64_t ca = 2 * pair;
@@ -495,7 +476,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     {
       float va[M];
       pcn_propose<float, M>(ua, sq, cs, bs, s.seed, ga, step, pc0, va, rw, (const float*)s.prior_chol, D);
-      oka = box_valid<float, M, LPC>(s, c0, va, lane);
+      oka = box_valid<float, M, LPC, IL>(s, c0, va, lane);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].x = va[j];
     }
@@ -503,7 +484,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
     {
       float vb[M];
       pcn_propose<float, M>(ub, sq, cs, bs, s.seed, gb, step, pc0, vb, rw, (const float*)s.prior_chol, D);
-      okb = has_b && box_valid<float, M, LPC>(s, c0, vb, lane);
+      okb = has_b && box_valid<float, M, LPC, IL>(s, c0, vb, lane);
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x].y = vb[j];
     }
@@ -515,9 +496,10 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
 #pragma unroll
       for (int j = 0; j < M; ++j) v[j] = vpark[j][threadIdx.x];
       const V reg = s.reg_scale
-                        ? regularizer<V, M, LPC, FM, float, kL96Block>((const float*)s.reg_scale + cl, v, lane, stage)
+                        ? regularizer<V, M, LPC, FM, float, kL96Block, IL>((const float*)s.reg_scale + cl, v, lane,
+                                                                         stage)
                         : V{0.f, 0.f};
-      V ph = l96_potential<V, M, LPC, FM>(v, (const float*)m.theta0 + cl, (const float*)m.x0 + cl,
+      V ph = l96_potential<V, M, LPC, FM, IL>(v, (const float*)m.theta0 + cl, (const float*)m.x0 + cl,
                                           (const float*)s.y + cl, (const float*)s.gamma_inv + cl, h, m.n_steps,
                                           lane, stage);
       if (s.reg_scale) ph = ph + reg;
@@ -588,9 +570,10 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
                                                               const T* __restrict__ yin,
                                                               const T* __restrict__ ginvin, T* __restrict__ out) {
   constexpr int M = D / LPC;
+  constexpr bool IL = (LPC == 8);  // interleaved groups of 8 (group_vlane)
   __shared__ T stage[PHI ? l96_stage_len<M, LPC>() : 1];
   const int lane = threadIdx.x & 63;
-  const int64_t tid = (int64_t)blockIdx.x * kL96Block + threadIdx.x;
+  const int64_t tid = (int64_t)blockIdx.x * kL96Block + group_vlane<LPC, IL>(threadIdx.x);
   const int64_t chain = tid / LPC;
   const int sub = (int)(tid % LPC);
   if (chain >= n) return;
@@ -603,13 +586,13 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
 #pragma unroll
   for (int j = 0; j < M; ++j) v[j] = u[j];
   if constexpr (PHI) {
-    const T ph = l96_potential<T, M, LPC, FM>(v, th0, x0, yin + c0, ginvin + c0, h, m.n_steps, lane, stage);
+    const T ph = l96_potential<T, M, LPC, FM, IL>(v, th0, x0, yin + c0, ginvin + c0, h, m.n_steps, lane, stage);
     if (sub == 0) out[chain] = ph;
   } else {
     T F[M], g[M];
 #pragma unroll
     for (int j = 0; j < M; ++j) F[j] = th0[j] + v[j];
-    l96_forward<T, M, LPC, FM>(F, x0, h, m.n_steps, lane, g);
+    l96_forward<T, M, LPC, FM, IL>(F, x0, h, m.n_steps, lane, g);
 #pragma unroll
     for (int j = 0; j < M; ++j) out[chain * D + c0 + j] = g[j];
   }

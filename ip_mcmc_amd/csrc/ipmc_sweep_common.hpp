@@ -80,17 +80,17 @@ __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __
 
 // s = Σ_i r_i^2 over the chain's q = LPC*M residuals in component order
 // (lane 0's M values, then lane 1's, ...), identical on every lane of the group.
-template <typename T, int M, int LPC, bool FM, int S = 0>
+template <typename T, int M, int LPC, bool FM, int S = 0, bool IL = false>
 __device__ __forceinline__ T ordered_sumsq(const T (&r)[M], int lane, T s) {
   if constexpr (S == LPC) {
     return s;
   } else {
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-      const T x = group_bcast<LPC, S>(r[j], lane);
+      const T x = group_bcast<LPC, S, IL>(r[j], lane);
       s = madd<FM>(x, x, s);
     }
-    return ordered_sumsq<T, M, LPC, FM, S + 1>(r, lane, s);
+    return ordered_sumsq<T, M, LPC, FM, S + 1, IL>(r, lane, s);
   }
 }
 
@@ -99,9 +99,9 @@ __device__ __forceinline__ T ordered_sumsq(const T (&r)[M], int lane, T s) {
 // lane of the group reads the chain's LPC*M values back in order -- broadcast
 // LDS reads instead of LPC*M cross-lane moves, which the compiler would issue
 // all at once and spill (d = 256: 345 VGPRs of spill without this).
-template <typename V, int M, int LPC, bool FM, int BLK>
+template <typename V, int M, int LPC, bool FM, int BLK, bool IL = false>
 __device__ __forceinline__ V ordered_sumsq_lds(const V (&r)[M], V* stage, V s) {
-  const int t = threadIdx.x;
+  const int t = group_vlane<LPC, IL>(threadIdx.x);  // the group's lanes are consecutive columns
   const int base = t & ~(LPC - 1);
 #pragma unroll
   for (int j = 0; j < M; ++j) stage[j * BLK + t] = r[j];
@@ -118,26 +118,26 @@ __device__ __forceinline__ V ordered_sumsq_lds(const V (&r)[M], V* stage, V s) {
   return s;
 }
 
-template <typename V, int M, int LPC, bool FM, int BLK>
+template <typename V, int M, int LPC, bool FM, int BLK, bool IL = false>
 __device__ __forceinline__ V group_sumsq(const V (&r)[M], int lane, V* stage, V s) {
-  if constexpr (LPC >= 8 && BLK > 0) return ordered_sumsq_lds<V, M, LPC, FM, BLK>(r, stage, s);
-  else return ordered_sumsq<V, M, LPC, FM>(r, lane, s);
+  if constexpr (LPC >= 8 && BLK > 0) return ordered_sumsq_lds<V, M, LPC, FM, BLK, IL>(r, stage, s);
+  else return ordered_sumsq<V, M, LPC, FM, 0, IL>(r, lane, s);
 }
 
 // StandardRWAccepter regularizer ½ Σ_i (c_i v_i)² over the chain's components
 // in component order (accepter.py:104-106 with the reference's sqrt-covariance
 // factor); c = reg_scale + this lane's offset.
-template <typename V, int M, int LPC, bool FM, typename S, int BLK = 0>
+template <typename V, int M, int LPC, bool FM, typename S, int BLK = 0, bool IL = false>
 __device__ __forceinline__ V regularizer(const S* __restrict__ c, const V (&v)[M], int lane, V* stage = nullptr) {
   using P = Splat<V>;
   V t[M];
 #pragma unroll
   for (int j = 0; j < M; ++j) t[j] = P::of(c[j]) * v[j];
-  return P::of((S)0.5) * group_sumsq<V, M, LPC, FM, BLK>(t, lane, stage, P::of((S)0));
+  return P::of((S)0.5) * group_sumsq<V, M, LPC, FM, BLK, IL>(t, lane, stage, P::of((S)0));
 }
 
 // ConstrainAccepter box: lo < v + off < hi for every component of the chain.
-template <typename T, int M, int LPC>
+template <typename T, int M, int LPC, bool IL = false>
 __device__ __forceinline__ bool box_valid(const ipmc_sweep& s, int c0, const T (&v)[M], int lane) {
   if (!s.box_lo && !s.box_hi) return true;
   const T* lo = (const T*)s.box_lo;
@@ -150,7 +150,7 @@ __device__ __forceinline__ bool box_valid(const ipmc_sweep& s, int c0, const T (
     if (lo && !(lo[c0 + j] < t)) ok = false;
     if (hi && !(t < hi[c0 + j])) ok = false;
   }
-  return group_all<LPC>(ok, lane);
+  return group_all<LPC, IL>(ok, lane);
 }
 
 // In-launch recording (ipmc_sweep.sample_every > 0, sampler.py:23-28): u

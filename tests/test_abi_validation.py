@@ -179,10 +179,10 @@ def test_auto_layout(h):
 # the in-place RK4 stages)
 LAYOUT_TABLE = [
     (8, "f64", 16384, 104), (8, "f64", 65536, 101), (8, "f32", 16384, 104), (8, "f32", 65536, 202),
-    (16, "f64", 16384, 104), (16, "f64", 65536, 101), (16, "f32", 16384, 104), (16, "f32", 65536, 202),
+    (16, "f64", 16384, 104), (16, "f64", 65536, 101), (16, "f32", 16384, 208), (16, "f32", 65536, 202),
     (40, "f64", 8192, 108), (40, "f64", 16384, 104), (40, "f64", 32768, 102), (40, "f64", 65536, 102),
-    (40, "f32", 8192, 108), (40, "f32", 16384, 104), (40, "f32", 32768, 204), (40, "f32", 65536, 202),
-    (80, "f64", 16384, 104), (80, "f64", 65536, 104), (80, "f32", 16384, 216), (80, "f32", 65536, 204),
+    (40, "f32", 8192, 108), (40, "f32", 16384, 208), (40, "f32", 32768, 204), (40, "f32", 65536, 202),
+    (80, "f64", 16384, 104), (80, "f64", 65536, 104), (80, "f32", 16384, 208), (80, "f32", 65536, 204),
     # below one wave per SIMD (speculative sweeps): DPP halos (profiles/r1/l96_small_layouts.jsonl)
     (40, "f64", 1, 104), (40, "f64", 64, 104), (40, "f64", 1024, 104), (40, "f32", 1, 104), (40, "f32", 1024, 104),
 ]
@@ -239,12 +239,16 @@ def test_plan_sweep_reports_what_the_sweep_runs(h):
     s.dtype = _abi.F32
     assert _plan(h, m, s) == (2, 2, 1)  # packed fp32 pairs
     s = _sweep(n=8192)
-    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 8192) == 108  # one step: LDS halos fill the GPU
+    assert h.ipmc_auto_layout(C.byref(m), _abi.F64, 8192) == 108  # 8 interleaved lanes fill the GPU
     assert _plan(h, m, s) == (8, 1, 1)
     s.n_steps = 16
-    assert _plan(h, m, s) == (4, 1, 2)  # multi-step: the DPP layout, 2 slots (one wave per SIMD)
+    assert _plan(h, m, s) == (8, 1, 1)  # short launches: sequential
+    s.n_steps = 512
+    assert _plan(h, m, s) == (4, 1, 2)  # long launches speculate on DPP quads, 2 slots (one wave per SIMD)
     s.dtype = _abi.F32
     assert _plan(h, m, s) == (4, 1, 2)  # fp32 the same
+    s.n_steps = 16
+    assert _plan(h, m, s) == (8, 1, 1)
     s.dtype = _abi.F64
     s3 = _sweep(n=32768)
     s3.n_steps = 2

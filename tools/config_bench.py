@@ -17,6 +17,7 @@ ts36     two-scale Lorenz-96 K=36 J=10, 2 000 RK4 steps of 0.
 """
 import ctypes as C
 import json
+import re
 import os
 import sys
 import time
@@ -87,14 +88,17 @@ def make(cfg):
     if cfg == "ts36":
         op = TwoScaleLorenz96Operator(K=36, J=10, dt=0.002, n_steps=2000, moments="mean")
         return op, 16384, 0.5, np.sqrt([10.0, 1.0, 10.0]), 45 * 396 * 2000, 0.5
-    if cfg.startswith("l96x"):
-        # the headline problem with few chains (the reference runs one): speculation territory
-        op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=2000)
-        return op, int(cfg[4:]), 0.2, np.ones(40), 30 * 40 * 2000, 0.1
+    if cfg.startswith("l96"):
+        # the headline problem with few chains (the reference runs one): speculation
+        # territory; "l96d80x16384": another dimension
+        mt = re.fullmatch(r"l96(?:d(\d+))?x(\d+)", cfg)
+        d = int(mt.group(1) or 40)
+        op = Lorenz96Operator(d, 8.0, dt=0.005, n_steps=2000)
+        return op, int(mt.group(2)), 0.2, np.ones(d), 30 * d * 2000, 0.1
     raise SystemExit(f"unknown config {cfg}")
 
 
-def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
+def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3, cpl=0):
     dev = torch.device("cuda", 0)
     op, n, beta, sq, flop, gamma = make(cfg)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
@@ -120,6 +124,7 @@ def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
         s.lanes_per_chain = lanes
     if spec is not None:
         s.spec_width = spec
+    s.chains_per_lane = cpl
     s.u, s.phi, s.accepts = u.data_ptr(), phi.data_ptr(), acc.data_ptr()
     s.y, s.gamma_inv, s.prior_sqrt = y.data_ptr(), gi.data_ptr(), sqt.data_ptr()
     s.beta, s.contraction = beta, float(np.sqrt(1 - beta**2))
@@ -169,11 +174,17 @@ def run(cfg, dtype, steps=10, lanes=0, per_launch=1, spec=None, warmup=3):
 if __name__ == "__main__":
     cfgs = sys.argv[1:] or ["cfg2", "cfg4", "cfg4full", "cfg4cfl", "cfg5"]
     # "cfg4:64" forces 64 lanes per chain (small models: speculation width), "cfg2@128" runs
-    # 128 pCN steps per launch, "l96x1~1" sets spec_width 1 (no speculation)
-    import re
-
+    # 128 pCN steps per launch, "l96x1~1" sets spec_width 1 (no speculation), "^2" two
+    # fp32 chains per lane group, "!f32" one dtype only
     for c in cfgs:
         name = re.match(r"[a-z0-9]+", c).group(0)
-        opt = {k: int(v) for k, v in re.findall(r"([:@~])(\d+)", c)}
-        for dt in (torch.float64, torch.float32):
-            run(name, dt, lanes=opt.get(":", 0), per_launch=opt.get("@", 1), spec=opt.get("~"))
+        opt = {k: int(v) for k, v in re.findall(r"([:@~^])(\d+)", c)}
+        dts = [torch.float64, torch.float32]
+        if "!f32" in c:
+            dts = [torch.float32]
+        elif "!f64" in c:
+            dts = [torch.float64]
+        for dt in dts:
+            if opt.get("^") and dt != torch.float32:
+                continue
+            run(name, dt, lanes=opt.get(":", 0), per_launch=opt.get("@", 1), spec=opt.get("~"), cpl=opt.get("^", 0))

@@ -51,6 +51,25 @@ case "$1" in
     done
     tools/gpu_session.sh "short:900:${cmds} true"
     ;;
+  p)  # LPC 8 halos by DPP (row_shr/row_shl + select) instead of ds_bpermute: parity, then the 8 192-chain shard
+    cmds=""
+    for K in "20 5" "200 10"; do set -- $K; k=$1; w=$2
+      for lw in "8 1" "4 2"; do set -- $lw
+        cmds="$cmds python bench.py --chains 8192 --lanes $1 --spec-width $2 --steps $k --warmup $w --no-cpu --no-extra >> gpurun_out/bench_8192_l8dpp.jsonl &&"
+      done
+    done
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "short:600:${cmds} true" \
+      "layouts:300:python tools/config_bench.py cfg5 l96x65536@1:8 > gpurun_out/configs_l8dpp.jsonl"
+    ;;
+  q)  # the LPC-8 interleaved layouts in the auto plan: parity, fp32 packed 8-lane layouts, the 8 192 shard
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "f32:400:python tools/config_bench.py 'l96x16384!f32' 'l96x16384:4^1!f32' 'l96d16x16384!f32' 'l96d16x16384:4^1!f32' 'l96d80x16384!f32' 'l96d80x16384:16^2!f32' > gpurun_out/layouts_l8il.jsonl" \
+      "f64:400:python tools/config_bench.py 'l96x8192!f64' 'l96x8192@512!f64' 'l96x8192@512:8~1!f64' 'l96d80x16384!f64' 'l96d16x16384!f64' >> gpurun_out/layouts_l8il.jsonl" \
+      "bench:600:python bench.py --chains 8192 --steps 20 --warmup 5 --no-cpu --no-extra > gpurun_out/bench_8192_auto.jsonl && python bench.py --chains 8192 --steps 200 --warmup 10 --no-cpu --no-extra >> gpurun_out/bench_8192_auto.jsonl && python bench.py --chains 8192 --steps 1024 --warmup 512 --no-cpu --no-extra >> gpurun_out/bench_8192_auto.jsonl && python bench.py --steps 20 --warmup 5 --no-cpu > gpurun_out/bench_65536_k20.jsonl"
+    ;;
   b)  # accept-path speculation (small models) and the K=6 two-scale layouts (SPL 3 DPP pairs / 1 / 6)
     V=ip_mcmc_amd/lib/variants
     tools/gpu_session.sh \
