@@ -93,6 +93,25 @@ class Workload:
         # the plan the sweep runs (ipmc_plan_sweep: same code path as the launch)
         self.lanes, self.chains_per_lane, self.spec_width = sweep_plan(self.model, s)
 
+    def settle_clocks(self, seconds):
+        """Untimed G evaluations of the chains' current u (ipmc_potential into a
+        scratch Φ: the chain state is untouched) for `seconds` of wall time, so
+        that a short timed region does not start on idle clocks (they ramp over
+        ~0.1-0.3 s of load: 65 536 chains ran 18.9 M steps/s at K = 20 after 5
+        warm-up steps, 20.4 M at K = 200; profiles/r3/bench_65536_k20.jsonl)."""
+        if seconds <= 0:
+            return
+        scratch = torch.empty_like(self.phi)
+        t0 = time.perf_counter()
+        i = 0
+        while time.perf_counter() - t0 < seconds:
+            call("ipmc_potential", C.byref(self.model), self.s.dtype, self.n_chains, self.u.data_ptr(),
+                 self.y.data_ptr(), self.ginv.data_ptr(), scratch.data_ptr(), self.stream)
+            i += 1
+            if i % 4 == 0:
+                torch.cuda.synchronize(self.dev)
+        torch.cuda.synchronize(self.dev)
+
     def launches(self, n_steps):
         """Launch sizes covering exactly n_steps pCN steps."""
         full, rem = divmod(n_steps, self.per_launch)
@@ -147,10 +166,13 @@ def max_over_ranks(x, world, dev):
     return x
 
 
-def timed(w, steps, warmup, world):
-    """Exactly `steps` pCN steps of every chain (after `warmup` untimed ones),
-    bracketed by barrier + synchronize; (max-rank wall seconds, mean kernel ms
-    per full launch of w.per_launch steps, from HIP events on the launch stream)."""
+def timed(w, steps, warmup, world, settle_s=0.0):
+    """Exactly `steps` pCN steps of every chain (after `warmup` untimed ones,
+    and settle_s seconds of untimed G evaluations that leave the chains as
+    they are), bracketed by barrier + synchronize; (max-rank wall seconds, mean
+    kernel ms per full launch of w.per_launch steps, from HIP events on the
+    launch stream)."""
+    w.settle_clocks(settle_s)
     for n in w.launches(warmup):
         w.step(n)
     torch.cuda.synchronize(w.dev)
@@ -280,6 +302,8 @@ def main():
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--spec-width", type=int, default=0, help="speculative slots per chain (0 = auto, 1 = off)")
+    ap.add_argument("--settle", type=float, default=0.3,
+                    help="seconds of untimed G evaluations before the warm-up steps (clock ramp; 0 = off)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -321,7 +345,7 @@ def main():
                  spec_width=args.spec_width)
     log(f"timing {args.steps} pCN steps ({args.dtype}, {per_rank} chains/GPU, {per_launch} steps/launch, "
         f"lanes={w.lanes}, spec_width={w.spec_width})")
-    el, kern_ms = timed(w, args.steps, args.warmup, world)
+    el, kern_ms = timed(w, args.steps, args.warmup, world, args.settle)
     log(f"{args.dtype}: {el:.3f} s, kernel {kern_ms:.3f} ms/launch")
     value = total_chains * args.steps / el
 
@@ -426,6 +450,7 @@ def main():
                 "chains_per_lane": w.chains_per_lane,
                 "spec_width": w.spec_width,
                 "parallelism": f"{total_chains} chains sharded over {world} GPU(s) ({args.scaling} scaling)",
+                "clock_settle_s": args.settle,
             },
             "roofline": {
                 "bound": "valu",

@@ -70,6 +70,10 @@ case "$1" in
       "f64:400:python tools/config_bench.py 'l96x8192!f64' 'l96x8192@512!f64' 'l96x8192@512:8~1!f64' 'l96d80x16384!f64' 'l96d16x16384!f64' >> gpurun_out/layouts_l8il.jsonl" \
       "bench:600:python bench.py --chains 8192 --steps 20 --warmup 5 --no-cpu --no-extra > gpurun_out/bench_8192_auto.jsonl && python bench.py --chains 8192 --steps 200 --warmup 10 --no-cpu --no-extra >> gpurun_out/bench_8192_auto.jsonl && python bench.py --chains 8192 --steps 1024 --warmup 512 --no-cpu --no-extra >> gpurun_out/bench_8192_auto.jsonl && python bench.py --steps 20 --warmup 5 --no-cpu > gpurun_out/bench_65536_k20.jsonl"
     ;;
+  r)  # short timed regions with the clock-settling pre-warm: N=1 and the N=8 shard, K = 20 / 200
+    tools/gpu_session.sh \
+      "bench:600:python bench.py --steps 20 --warmup 5 --no-cpu --no-extra > gpurun_out/bench_settle.jsonl && python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --settle 0 >> gpurun_out/bench_settle.jsonl && python bench.py --chains 8192 --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl && python bench.py --chains 8192 --steps 200 --warmup 10 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl && python bench.py --chains 16384 --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl && python bench.py --chains 32768 --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl"
+    ;;
   b)  # accept-path speculation (small models) and the K=6 two-scale layouts (SPL 3 DPP pairs / 1 / 6)
     V=ip_mcmc_amd/lib/variants
     tools/gpu_session.sh \
