@@ -266,10 +266,12 @@ def e2e_run(op, y, n_chains, chain_offset, dtype_np, dev, world, n_samples=20):
 
     prior = GaussianDistribution(np.zeros(D), np.eye(D))
     pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(D), GAMMA**2 * np.eye(D)))
-    u0 = np.zeros((n_chains, D))
+    u0 = np.full((n_chains, D), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch, inside run())
     s = MCMCSampler(ConstSteppCNProposer(BETA, prior), pCNAccepter(pot), PhiloxRNG(2), dtype=dtype_np, device=dev,
                     chain_offset=chain_offset)
-    s.run(u0, n_samples=2, burn_in=1, sample_interval=1)  # warm: allocations, page-locked pool
+    # warm run of the same size: device allocations, and the page-locked result
+    # block that torch's host allocator recycles once the caller drops it
+    s.run(u0, n_samples=n_samples, burn_in=1, sample_interval=1)
     torch.cuda.synchronize(dev)
     barrier(world)
     t0 = time.perf_counter()

@@ -366,8 +366,10 @@ class MCMCSampler:
         copies = []  # (first sample, end sample, event after its sweeps)
         src64 = None
         if overlap:
-            n_blk = min(n_samples, OVERLAP_COPY_BLOCKS)
-            bounds = [(j + 1) * n_samples // n_blk for j in range(n_blk)]
+            # the last block is one sample: its copy is all that is left after
+            # the sweeps (blocks of ~n/8 samples before it)
+            n_blk = min(n_samples - 1, OVERLAP_COPY_BLOCKS - 1)
+            bounds = [(j + 1) * (n_samples - 1) // n_blk for j in range(n_blk)] + [n_samples]
             if td != torch.float64:
                 # f64 staging for the converted blocks, allocated before any sweep
                 # is queued so that no block still in use is handed back to us

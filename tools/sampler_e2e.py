@@ -33,8 +33,10 @@ def main():
         for keep in ("samples", "moments"):
             acc = CountedAccepter(pCNAccepter(pot))
             s = MCMCSampler(ConstSteppCNProposer(B.BETA, prior), acc, PhiloxRNG(2), dtype=dtype)
-            s.run(np.zeros((chains, d)), n_samples=1, burn_in=0, sample_interval=1, keep=keep)  # warm-up
-            u0 = np.zeros((chains, d))
+            # warm-up of the same size: the page-locked result buffer of a run is
+            # recycled by torch's host allocator once the caller drops it
+            s.run(np.zeros((chains, d)), n_samples=n_samples, burn_in=interval, sample_interval=interval, keep=keep)
+            u0 = np.full((chains, d), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch, inside run())
             t0 = time.perf_counter()
             out = s.run(u0, n_samples=n_samples, burn_in=interval, sample_interval=interval, keep=keep)
             wall = time.perf_counter() - t0

@@ -74,6 +74,29 @@ case "$1" in
     tools/gpu_session.sh \
       "bench:600:python bench.py --steps 20 --warmup 5 --no-cpu --no-extra > gpurun_out/bench_settle.jsonl && python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --settle 0 >> gpurun_out/bench_settle.jsonl && python bench.py --chains 8192 --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl && python bench.py --chains 8192 --steps 200 --warmup 10 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl && python bench.py --chains 16384 --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl && python bench.py --chains 32768 --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_settle.jsonl"
     ;;
+  s)  # where MCMCSampler.run's end-to-end time goes: kernel + memory-copy trace of the e2e workload
+    tools/gpu_session.sh \
+      "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_plain.jsonl" \
+      "trace:300:timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/e2e_trace -o run -- python tools/sampler_e2e.py 65536 20 1"
+    ;;
+  t)  # e2e after the one-sample last copy block and a same-size warm-up; the bench line
+    tools/gpu_session.sh \
+      "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_t.jsonl && python tools/sampler_e2e.py 65536 20 5 >> gpurun_out/e2e_t.jsonl" \
+      "trace:300:timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/e2e_trace_t -o run -- python tools/sampler_e2e.py 65536 20 1" \
+      "bench:400:python bench.py > gpurun_out/bench_line_t.json"
+    ;;
+  w)  # the parity suite, then e2e with page-locked H2D staging, its host profile and the bench line
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_w.jsonl && python tools/probes/e2e_host_profile.py > gpurun_out/e2e_host_profile_w.txt" \
+      "bench:400:python bench.py > gpurun_out/bench_line_w.json"
+    ;;
+  x)  # H2D staging probe
+    tools/gpu_session.sh "h2d:200:python tools/probes/h2d_probe.py > gpurun_out/h2d_probe.txt"
+    ;;
+  u)  # host-side profile of MCMCSampler.run (e2e)
+    tools/gpu_session.sh "prof:300:python tools/probes/e2e_host_profile.py 65536 20 1 moments > gpurun_out/e2e_host_profile_moments.txt && python tools/probes/e2e_host_profile.py 65536 20 1 samples > gpurun_out/e2e_host_profile_samples.txt"
+    ;;
   b)  # accept-path speculation (small models) and the K=6 two-scale layouts (SPL 3 DPP pairs / 1 / 6)
     V=ip_mcmc_amd/lib/variants
     tools/gpu_session.sh \
