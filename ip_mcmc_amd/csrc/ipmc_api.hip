@@ -101,8 +101,9 @@ static bool l96_has(int D, int dtype, int lpc, int cpl) {
 //  3. else (an ensemble below one wave per SIMD, where the speculative sweep
 //     fills lanes with slots) the most DPP lanes per chain that keep >= 4
 //     components per lane: a chain's RK4 step is then a latency chain, and
-//     LDS halos made it 1.6x slower (d=40 at 1 / 64 / 1 024 chains: LPC 4
-//     0.050 / 0.050 / 0.054 ms per step vs LPC 8 0.080 / 0.084 / 0.087).
+//     LPC 8 (round 1, halos through LDS) was 1.6x slower (d=40 at 1 / 64 /
+//     1 024 chains: LPC 4 0.050 / 0.050 / 0.054 ms per step vs LPC 8 0.080 /
+//     0.084 / 0.087).
 // The most lanes per chain whose halos go by DPP (LPC 1, 2, 4, 16) with >= 4
 // components per lane, 0 if none is compiled: the layout of latency-bound
 // chains (small ensembles, speculative slots).
