@@ -168,7 +168,7 @@ case "$1" in
       "write32:200:timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc32/write -o run -- $B --dtype f32" \
       "sq32:200:timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc32/sq -o run -- $B --dtype f32" \
       "summ:60:python tools/pmc_summarize.py gpurun_out/pmc64 f64 65536 gpurun_out/pmc_l96_f64.json && python tools/pmc_summarize.py gpurun_out/pmc32 f32 65536 gpurun_out/pmc_l96_f32.json" \
-      "shard8k:600:for l in 64 128 256 512; do python bench.py --chains 8192 --steps-per-launch \$l --steps 512 --warmup 16 --no-cpu --no-extra >> gpurun_out/bench_8192_long.jsonl || exit 3; done" \
+      "shards:600:for c in 32768 16384 8192; do python bench.py --chains \$c --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_shards_k20.jsonl || exit 3; done" \
       "bench_strong:600:python bench.py --chains 16384 --no-cpu > gpurun_out/bench_16384.json && python bench.py --chains 8192 --no-cpu > gpurun_out/bench_8192.json"
     ;;
   *) echo "unknown session $1"; exit 2 ;;
