@@ -209,6 +209,32 @@ def test_sweep_l96_bit_exact_every_layout(dev, orc, dtype, cpl, K, lanes):
         assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
 
 
+@pytest.mark.parametrize("dtype,cpl", [(torch.float64, 1), (torch.float32, 1), (torch.float32, 2)])
+@pytest.mark.parametrize("K", [16, 40, 80])
+def test_sweep_l96_interleaved_8_lanes_box_rw_schedule(dev, orc, dtype, cpl, K):
+    """8 lanes per chain run two chains interleaved per 16-lane row
+    (group_vlane): the box's group vote, the RW regularizer's and the misfit's
+    LDS-staged in-order sums and the halos all follow the interleaved lanes.
+    131 chains: the last row's odd lanes (and a packed pair's partner) are
+    phantoms."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    if (dtype == torch.float64 or cpl == 2) and K // 8 > 20:
+        pytest.skip("no 8-byte-storage instantiation with more than 20 components per lane")
+    n = 9
+    sched = np.stack([np.linspace(0.05, 0.4, n), np.sqrt(1 - np.linspace(0.05, 0.4, n) ** 2)], axis=1)
+    op = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=40)
+    U0, phi0, y, ginv, sq = _problem(op, 131, dtype, orc, seed=K + 1)
+    box = (np.full(K, -0.6), np.full(K, 0.7), np.linspace(-0.05, 0.05, K))
+    rs = np.linspace(0.5, 2.0, K)
+    phr = orc.init_phi(op, U0.astype(_np(dtype)), y, ginv, reg_scale=rs).astype(np.float64)
+    for kw, ph in ((dict(box=box, sched=sched), phi0), (dict(proposal="rw", reg_scale=rs, box=box), phr)):
+        o = _sweep_oracle(orc, op, U0, ph, y, ginv, sq, 0.2, 13, 3, n, dtype, **kw)
+        assert 0 < o["acc"].sum() < 131 * n
+        d = _sweep_device(op, U0, ph, y, ginv, sq, 0.2, 13, 3, n, dtype, dev, lanes=8, cpl=cpl, spec=1, **kw)
+        _assert_same(d, o, (K, str(dtype), cpl, sorted(kw)))
+
+
 def test_sweep_l96_d256_subset_bit_exact(dev, orc):
     """Config 5 shape at reduced length (d=256, 500 RK4 steps, 4096 chains), auto layouts."""
     from ip_mcmc_amd import Lorenz96Operator

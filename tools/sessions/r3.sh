@@ -94,6 +94,9 @@ case "$1" in
   x)  # H2D staging probe
     tools/gpu_session.sh "h2d:200:python tools/probes/h2d_probe.py > gpurun_out/h2d_probe.txt"
     ;;
+  y)  # the interleaved 8-lane layout with box / RW regularizer / schedule, and the fuzz
+    tools/gpu_session.sh "il8:600:$PYT -q tests/test_gpu_parity.py tests/test_gpu_fuzz.py -k 'interleaved or fuzz or every_layout' -m gpu"
+    ;;
   u)  # host-side profile of MCMCSampler.run (e2e)
     tools/gpu_session.sh "prof:300:python tools/probes/e2e_host_profile.py 65536 20 1 moments > gpurun_out/e2e_host_profile_moments.txt && python tools/probes/e2e_host_profile.py 65536 20 1 samples > gpurun_out/e2e_host_profile_samples.txt"
     ;;
