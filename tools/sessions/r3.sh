@@ -97,6 +97,9 @@ case "$1" in
   y)  # the interleaved 8-lane layout with box / RW regularizer / schedule, and the fuzz
     tools/gpu_session.sh "il8:600:$PYT -q tests/test_gpu_parity.py tests/test_gpu_fuzz.py -k 'interleaved or fuzz or every_layout' -m gpu"
     ;;
+  z)  # the reference's config-1 script through the host step (one-chain float loop)
+    tools/gpu_session.sh "stuart:400:python examples/stuart_reference.py > gpurun_out/stuart_reference.jsonl"
+    ;;
   u)  # host-side profile of MCMCSampler.run (e2e)
     tools/gpu_session.sh "prof:300:python tools/probes/e2e_host_profile.py 65536 20 1 moments > gpurun_out/e2e_host_profile_moments.txt && python tools/probes/e2e_host_profile.py 65536 20 1 samples > gpurun_out/e2e_host_profile_samples.txt"
     ;;
