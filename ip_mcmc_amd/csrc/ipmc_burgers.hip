@@ -7,7 +7,8 @@
 // nlive hold no cells).  The ghost cells are explicit values on the first and
 // last live lane (the IC sets them, rusanov.py:32, and the first step reads
 // them before any boundary condition is applied).  Interface fluxes between
-// lanes use the neighbour lane's edge cell (ds_bpermute); each lane computes
+// lanes use the neighbour lane's edge cell (DPP wave_shr:1 / wave_shl:1,
+// below); each lane computes
 // CPL+1 fluxes, the shared edge flux bit-identically on both sides.  CFL mode
 // reduces max|w| over the group every step (exact, order-free); fixed-dt mode
 // keeps a per-lane guard and reduces once.  The final interior state is staged
