@@ -176,7 +176,8 @@ def test_auto_layout(h):
 # (dim, dtype, chains) -> cpl * 100 + lpc: the measured-fastest layout, or one
 # within 4 % of it, of profiles/r1/lanes_layout_rule.txt (d=40 at 32 768 and
 # 65 536 chains: profiles/r2/lanes_inplace.txt, lanes_scan_d40_r2k.txt, after
-# the in-place RK4 stages)
+# the in-place RK4 stages; fp32 at 16 384 chains on 8 interleaved lanes x 2
+# chains: profiles/r3/layouts_l8il.jsonl)
 LAYOUT_TABLE = [
     (8, "f64", 16384, 104), (8, "f64", 65536, 101), (8, "f32", 16384, 104), (8, "f32", 65536, 202),
     (16, "f64", 16384, 104), (16, "f64", 65536, 101), (16, "f32", 16384, 208), (16, "f32", 65536, 202),
