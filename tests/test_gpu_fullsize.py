@@ -156,3 +156,38 @@ def test_cfg2_full_shape(dev, orc, dtype):
         assert np.array_equal(d[key], o[key]), key
     rate = o["acc"].sum() / (C_ * n)
     assert 0.01 < rate < 0.99, rate
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_strong_scaled_8gpu_shard_both_plans(dev, orc, dtype):
+    """The 8-GPU shard of the headline (8 192 chains of d=40, the last rank's
+    global ids) under both automatic plans: a short launch runs sequentially on
+    8 interleaved lanes, a >= 256-step launch speculates on 4 lanes x 2 slots
+    (ipmc_plan_sweep); every chain equals the oracle's sequential chain.  The
+    forward map is shortened to 20 RK4 steps so the oracle checks all chains
+    in seconds; the bench problem's burn-in from u = 0 (y from the forcing
+    field F = 8 + 0.5 sin) makes acceptances frequent early on."""
+    import ctypes as C
+
+    from ip_mcmc_amd import Lorenz96Operator, _abi
+    from ip_mcmc_amd._lib import call
+
+    op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=20)
+    C_, off = 8192, 7 * 8192
+    k = np.arange(40)
+    y = orc.forward(op, (0.5 * np.sin(2 * np.pi * k / 40))[None, :])[0] + 0.1 * np.random.default_rng(3).normal(size=40)
+    ginv, sq = np.full(40, 10.0), np.ones(40)
+    U0 = np.zeros((C_, 40))
+    phi0 = _device_phi(op, U0, y, ginv, dtype, dev).astype(np.float64)
+    m, _ = op.model(dtype, dev)
+    for n, want in ((16, (8, 1, 1)), (256, (4, 1, 2))):
+        sw = _abi.IpmcSweep()
+        sw.dtype, sw.n_chains, sw.n_steps, sw.spec_width = (_abi.F64 if dtype == torch.float64 else _abi.F32), C_, n, 0
+        plan = _abi.IpmcPlan()
+        call("ipmc_plan_sweep", C.byref(m), C.byref(sw), C.byref(plan))
+        assert (plan.lanes_per_chain, plan.chains_per_lane, plan.spec_width) == want
+        d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.2, 2, 0, n, dtype, dev, spec=0, chain_offset=off)
+        o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.2, 2, 0, n, dtype, chain_offset=off)
+        for key in ("u", "phi", "acc"):
+            assert np.array_equal(d[key], o[key]), (n, key)
+        assert 0 < o["acc"].sum() < C_ * n

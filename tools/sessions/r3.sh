@@ -94,6 +94,9 @@ case "$1" in
   x)  # H2D staging probe
     tools/gpu_session.sh "h2d:200:python tools/probes/h2d_probe.py > gpurun_out/h2d_probe.txt"
     ;;
+  y2)  # the 8-GPU shard under both plans vs the oracle
+    tools/gpu_session.sh "shard:600:$PYT -v tests/test_gpu_fullsize.py -k strong_scaled -m gpu"
+    ;;
   y)  # the interleaved 8-lane layout with box / RW regularizer / schedule, and the fuzz
     tools/gpu_session.sh "il8:600:$PYT -q tests/test_gpu_parity.py tests/test_gpu_fuzz.py -k 'interleaved or fuzz or every_layout' -m gpu"
     ;;
