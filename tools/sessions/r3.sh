@@ -94,6 +94,11 @@ case "$1" in
   x)  # H2D staging probe
     tools/gpu_session.sh "h2d:200:python tools/probes/h2d_probe.py > gpurun_out/h2d_probe.txt"
     ;;
+  bq)  # Burgers config 4 per-GPU share (2 048 chains): SQ pass and the layouts
+    tools/gpu_session.sh \
+      "sq:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_cfg4 -o run -- python tools/config_bench.py cfg4" \
+      "layouts:300:python tools/config_bench.py cfg4 cfg4:16 cfg4:64 cfg4visc cfg4cfl > gpurun_out/cfg4_layouts.jsonl"
+    ;;
   y2)  # the 8-GPU shard under both plans vs the oracle
     tools/gpu_session.sh "shard:600:$PYT -v tests/test_gpu_fullsize.py -k strong_scaled -m gpu"
     ;;
