@@ -79,6 +79,11 @@ def make(cfg):
             op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000)
         n = 16384 if cfg == "cfg4full" else 2048
         return op, n, 0.15, np.full(3, 0.25), 30 * 256 * 1000, 0.05
+    mt = re.fullmatch(r"cfg4n(\d+)", cfg)
+    if mt:  # config 4's share with another number of fixed time steps (per-pCN-step overhead fits)
+        nst = int(mt.group(1))
+        op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=nst)
+        return op, 2048, 0.15, np.full(3, 0.25), 30 * 256 * nst, 0.05
     if cfg == "cfg5":
         op = Lorenz96Operator(256, 8.0, dt=0.005, n_steps=10000)
         return op, 131072, 0.2, np.ones(256), 30 * 256 * 10000, 0.1

@@ -99,6 +99,9 @@ case "$1" in
       "sq:200:timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d gpurun_out/sq_cfg4 -o run -- python tools/config_bench.py cfg4" \
       "layouts:300:python tools/config_bench.py cfg4 cfg4:16 cfg4:64 cfg4visc cfg4cfl > gpurun_out/cfg4_layouts.jsonl"
     ;;
+  bn)  # Burgers config 4 share at 250 / 500 / 1000 / 2000 time steps: the per-pCN-step overhead
+    tools/gpu_session.sh "fit:300:python tools/config_bench.py cfg4n250 cfg4n500 cfg4n1000 cfg4n2000 > gpurun_out/cfg4_nsteps.jsonl"
+    ;;
   y2)  # the 8-GPU shard under both plans vs the oracle
     tools/gpu_session.sh "shard:600:$PYT -v tests/test_gpu_fullsize.py -k strong_scaled -m gpu"
     ;;
