@@ -463,13 +463,13 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
-  const bool prior = spec_accept_prior(s, chain);  // the speculated path (ipmc_sweep_common.hpp)
+  SpecGuess guess(spec_accept_prior(s, chain));  // the speculated path (ipmc_sweep_common.hpp)
   const bool rw = s.proposal == IPMC_PROPOSAL_RW;
   const T* chol = (const T*)s.prior_chol;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + slot;
-    const bool amode = S > 1 && spec_accept_mode(st, nacc, prior);
+    const bool amode = S > 1 && guess.accept_mode();
     bool ok = false;
     T phv = (T)0;
     double lr = 0.0;
@@ -610,6 +610,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
       phu = phf;
     }
     nacc += rd.nar;
+    guess.settle(rd.nar, rd.used);
     st += rd.used;
   }
   if (r == 0) {

@@ -278,11 +278,11 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
-  const bool prior = spec_accept_prior(s, chain);  // the speculated path (ipmc_sweep_common.hpp)
+  SpecGuess guess(spec_accept_prior(s, chain));  // the speculated path (ipmc_sweep_common.hpp)
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + slot;
-    const bool amode = spec_accept_mode(st, nacc, prior);
+    const bool amode = guess.accept_mode();
     bool ok = false;
     T phv = (T)0;
     double lr = 0.0;
@@ -408,6 +408,7 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
       phu = phf;
     }
     nacc += rd.nar;
+    guess.settle(rd.nar, rd.used);
     if (G <= 64) wave_sync_lds();  // the parks are rewritten next round
     else __syncthreads();
     st += rd.used;

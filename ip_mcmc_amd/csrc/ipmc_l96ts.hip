@@ -512,12 +512,12 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
-  const bool prior = spec_accept_prior(s, chain);
+  SpecGuess guess(spec_accept_prior(s, chain));
   const T* chol = (const T*)s.prior_chol;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + slot;
-    const bool amode = S > 1 && spec_accept_mode(st, nacc, prior);
+    const bool amode = S > 1 && guess.accept_mode();
     int kq = c.sub;
     asm volatile("" : "+v"(kq));
     bool ok = false, acc = false;
@@ -631,6 +631,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
       phu = phf;
     }
     nacc += rd.nar;
+    guess.settle(rd.nar, rd.used);
     st += rd.used;
   }
   if (r == 0) {

@@ -343,18 +343,17 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   // the proposals of the slots before it from their draws in the sequential
   // order -- and the first rejection ends the round; the mismatching slot's own
   // decision is valid (its inputs were right), so a round settles up to S
-  // steps either way.  A chain runs accept mode while it accepts at least half
-  // of this launch's steps (at its first round: its accept counter over the
-  // global steps before the launch, if any).  Config 2 accepts 88 %: reject
+  // steps either way.  A chain runs accept mode while it accepted at least half
+  // of its recent steps (SpecGuess; at its first round: its accept counter over
+  // the global steps before the launch, if any).  Config 2 accepts 88 %: reject
   // mode settles ~1.1 steps per round there, accept mode ~1/(1-p) = 8.
-  const int64_t hist_acc = s.accepts ? s.accepts[chain] : 0;
-  const bool prior_accept = !s.accepts || s.step0 == 0 || (uint64_t)(2 * hist_acc) >= s.step0;
+  SpecGuess guess(spec_accept_prior(s, chain));
   T* wown = wpark + t;                    // this lane's proposal noise, wown[j * kSpecBlock] (accept mode)
   const T* wgroup = wpark + (t - sub);
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int64_t tt = st + sub;
-    const bool amode = st == 0 ? prior_accept : 2 * nacc >= st;
+    const bool amode = guess.accept_mode();
     if constexpr (PRE) {
       // refill when this round's slots reach past the held draws (uniform per group)
       if (st + S > pend && pend < s.n_steps) {
@@ -510,6 +509,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       phu = phf;
     }
     nacc += nar;
+    guess.settle(nar, used);
     wave_sync_lds();  // the parks are rewritten next round
     st += used;
   }

@@ -184,15 +184,37 @@ struct SampleClock {
 // from slot s-1's proposal, the first rejection ends the round).  The slot
 // where the guess first fails still decided correctly (its inputs were
 // right), so a round settles `used` steps either way and the results are
-// bit-identical to the sequential chain; the guess only changes how many.  A
-// chain guesses "accept" while it accepts at least half of this launch's
-// steps; before its first round, `prior`.
-__device__ __forceinline__ bool spec_accept_mode(int64_t st, int64_t nacc, bool prior) {
+// bit-identical to the sequential chain; the guess only changes how many.
+// A chain guesses "accept" while it accepted at least half of its recent
+// steps: accepted and settled steps summed over its rounds with weight 3/4 per
+// round back (~4 rounds).  Rounds 1-3 used the whole launch's ratio, which
+// lags behind a posterior whose acceptance changes along the run (burn-in, a
+// step-size schedule) once launches are long (sampler.STEPS_PER_LAUNCH).
+// Before its first round: `prior`.
+struct SpecGuess {
+  float a, n;  // recency-weighted accepted / settled steps
+  __device__ __forceinline__ explicit SpecGuess(bool prior) : a(prior ? 1.f : 0.f), n(1.f) {}
+  __device__ __forceinline__ bool accept_mode() const {
 #ifdef IPMC_SPEC_REJECT_ONLY  // experiments (tools/build_variant.sh): the reject path only
-  return false;
+    return false;
 #endif
-  return st == 0 ? prior : 2 * nacc >= st;
-}
+    return 2.f * a >= n;
+  }
+  __device__ __forceinline__ void settle(int nar, int used) {
+#ifdef IPMC_SPEC_GUESS_CUMULATIVE  // experiments: rounds 1-3's whole-launch ratio
+    if (fresh) a = n = 0.f;
+    fresh = false;
+    a += (float)nar;
+    n += (float)used;
+#else
+    a = fmaf(0.75f, a, (float)nar);
+    n = fmaf(0.75f, n, (float)used);
+#endif
+  }
+#ifdef IPMC_SPEC_GUESS_CUMULATIVE
+  bool fresh = true;
+#endif
+};
 // The prior at a launch's first round: the chain's accept counter over the
 // global steps before the launch (accept mode without any history).
 __device__ __forceinline__ bool spec_accept_prior(const ipmc_sweep& s, int64_t chain) {

@@ -41,7 +41,11 @@ from .rng import PhiloxRNG, resolve_rng
 
 # pCN steps per chain in one kernel launch (launches are split at sample
 # boundaries; this bounds a single launch's run time for large ensembles).
-STEPS_PER_LAUNCH = 1024
+# A speculative launch lasts as long as its slowest chain takes to settle the
+# launch's steps, and that excess over the mean shrinks with the launch
+# length: config 2 (4 096 chains, 88 % accepted) runs 323 / 403 / 447 M steps/s
+# at 1 024 / 4 096 / 16 384 steps per launch (profiles/r3/launch_len.jsonl).
+STEPS_PER_LAUNCH = 16384
 # ... and fewer for heavy ensembles: about LAUNCH_WORK state-component updates
 # per launch (~0.5 s on one MI355X; the headline sweep is 5.2e9 per step).
 LAUNCH_WORK = 8e11

@@ -191,3 +191,42 @@ def test_strong_scaled_8gpu_shard_both_plans(dev, orc, dtype):
         for key in ("u", "phi", "acc"):
             assert np.array_equal(d[key], o[key]), (n, key)
         assert 0 < o["acc"].sum() < C_ * n
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_cfg2_long_launch_equals_short_launches(dev, orc, dtype):
+    """Config 2 at the sampler's launch length (sampler.STEPS_PER_LAUNCH =
+    16 384 for this ensemble): one 4 096-step launch -- each chain settles its
+    steps in its own number of speculative rounds while the launch waits for
+    the slowest -- equals 32 launches of 128 steps for all 4 096 chains (state,
+    Φ, accept and call counts), and 8 chains equal the oracle's sequential
+    chain over the 4 096 steps."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import config_bench as CB
+    from ip_mcmc_amd.sampler import _steps_per_launch
+
+    op, y, ginv, sq, beta = CB.cfg2_problem()
+    m, _ = op.model(dtype, dev)
+    assert _steps_per_launch(m, 4096) == 16384
+    C_, n, short = 4096, 4096, 128
+    rng = np.random.default_rng(23)
+    U0 = (sq * rng.normal(size=(C_, 3))).astype(_np(dtype)).astype(np.float64)
+    phi0 = _device_phi(op, U0, y, ginv, dtype, dev).astype(np.float64)
+    a = _sweep_device(op, U0, phi0, y, ginv, sq, beta, 4, 0, n, dtype, dev, spec=0)
+    b = dict(u=U0, phi=phi0, acc=np.zeros(C_, dtype=np.int64), calls=np.zeros(C_, dtype=np.int64))
+    for st in range(0, n, short):
+        r = _sweep_device(op, b["u"], b["phi"], y, ginv, sq, beta, 4, st, short, dtype, dev, spec=0)
+        b = dict(u=r["u"].astype(np.float64), phi=r["phi"].astype(np.float64), acc=b["acc"] + r["acc"],
+                 calls=b["calls"] + r["calls"])
+    for key in ("u", "phi", "acc", "calls"):
+        assert np.array_equal(np.asarray(a[key], dtype=np.float64), np.asarray(b[key], dtype=np.float64)), key
+    idx = np.array([0, 1, 777, 2048, 3000, 4000, 4094, 4095])
+    for i in idx:
+        o = _sweep_oracle(orc, op, U0[i:i + 1], phi0[i:i + 1], y, ginv, sq, beta, 4, 0, n, dtype, chain_offset=int(i))
+        for key in ("u", "phi", "acc", "calls"):
+            assert np.array_equal(a[key][i], o[key][0]), (i, key)
+    rate = a["acc"].sum() / (C_ * n)
+    assert 0.5 < rate < 0.99, rate

@@ -188,5 +188,23 @@ case "$1" in
       "shards:600:for c in 32768 16384 8192; do python bench.py --chains \$c --steps 20 --warmup 5 --no-cpu --no-extra >> gpurun_out/bench_shards_k20.jsonl || exit 3; done" \
       "bench_strong:600:python bench.py --chains 16384 --no-cpu > gpurun_out/bench_16384.json && python bench.py --chains 8192 --no-cpu > gpurun_out/bench_8192.json"
     ;;
+  ll)  # launch length vs the slowest chain: speculative ensembles at 1 024 / 4 096 / 16 384 steps per launch
+    tools/gpu_session.sh \
+      "cfg2:400:python tools/config_bench.py cfg2@1024 cfg2@4096 cfg2@16384 > gpurun_out/launch_len.jsonl" \
+      "l96:400:python tools/config_bench.py 'l96x1024@1024!f64' 'l96x1024@8192!f64' 'l96x64@1024!f64' 'l96x64@8192!f64' >> gpurun_out/launch_len.jsonl"
+    ;;
+  lm)  # the sampler at 16 384 steps per launch: the long-launch test, the reference studies through run()
+    tools/gpu_session.sh \
+      "tests:600:$PYT -v tests/test_gpu_fullsize.py tests/test_gpu_run.py -k 'cfg2 or run or interval' -m gpu" \
+      "examples:500:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/burgers_beta.py > gpurun_out/example_burgers_beta.jsonl && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl"
+    ;;
+  sg)  # speculation guess over recent rounds (SpecGuess) vs the whole launch's ratio (variants/cum)
+    V=ip_mcmc_amd/lib/variants/cum/libipmc.so
+    tools/gpu_session.sh \
+      "tests:600:$PYT -q tests/test_gpu_fullsize.py tests/test_gpu_run.py tests/test_gpu_fuzz.py tests/test_gpu_parity.py tests/test_gpu_ts_layout.py -k 'cfg2 or run or interval or fuzz or speculative or ts_' -m gpu" \
+      "ex_new:300:python examples/burgers_beta.py > gpurun_out/guess_burgers_new.jsonl && python examples/lorenz_thesis.py > gpurun_out/guess_thesis_new.json" \
+      "ex_cum:300:IPMC_LIB_PATH=$V python examples/burgers_beta.py > gpurun_out/guess_burgers_cum.jsonl && IPMC_LIB_PATH=$V python examples/lorenz_thesis.py > gpurun_out/guess_thesis_cum.json" \
+      "cfg2:300:python tools/config_bench.py cfg2@16384 cfg2@1024 > gpurun_out/guess_cfg2_new.jsonl && IPMC_LIB_PATH=$V python tools/config_bench.py cfg2@16384 cfg2@1024 > gpurun_out/guess_cfg2_cum.jsonl"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
