@@ -206,5 +206,10 @@ case "$1" in
       "ex_cum:300:IPMC_LIB_PATH=$V python examples/burgers_beta.py > gpurun_out/guess_burgers_cum.jsonl && IPMC_LIB_PATH=$V python examples/lorenz_thesis.py > gpurun_out/guess_thesis_cum.json" \
       "cfg2:300:python tools/config_bench.py cfg2@16384 cfg2@1024 > gpurun_out/guess_cfg2_new.jsonl && IPMC_LIB_PATH=$V python tools/config_bench.py cfg2@16384 cfg2@1024 > gpurun_out/guess_cfg2_cum.jsonl"
     ;;
+  c2)  # config 2 through MCMCSampler.run; a 65 536-step launch (the slowest-chain bound)
+    tools/gpu_session.sh \
+      "example:300:python examples/lorenz63_config2.py > gpurun_out/example_lorenz63_config2.jsonl" \
+      "cfg2:300:python tools/config_bench.py cfg2@16384 cfg2@65536 > gpurun_out/launch_len_65536.jsonl"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
