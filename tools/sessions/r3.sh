@@ -211,5 +211,11 @@ case "$1" in
       "example:300:python examples/lorenz63_config2.py > gpurun_out/example_lorenz63_config2.jsonl" \
       "cfg2:300:python tools/config_bench.py cfg2@16384 cfg2@65536 > gpurun_out/launch_len_65536.jsonl"
     ;;
+  ps)  # page-locked asynchronous copy of the final chain state: the suite, e2e, the bench line
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q" \
+      "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_ps.jsonl" \
+      "bench:400:python bench.py > gpurun_out/bench_line_ps.json"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
