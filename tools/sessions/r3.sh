@@ -217,5 +217,14 @@ case "$1" in
       "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_ps.jsonl" \
       "bench:400:python bench.py > gpurun_out/bench_line_ps.json"
     ;;
+  sk)  # the 8 192-chain shard at K = 20 vs 200: per-dispatch kernel times
+    tools/gpu_session.sh \
+      "k20:200:timeout -k 10 150 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/shard_k20 -o run -- python bench.py --chains 8192 --steps 20 --warmup 5 --no-cpu --no-extra" \
+      "k200:200:timeout -k 10 150 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/shard_k200 -o run -- python bench.py --chains 8192 --steps 200 --warmup 10 --no-cpu --no-extra"
+    ;;
+  fc)  # final-tree config table (every config on one box)
+    tools/gpu_session.sh \
+      "configs:600:python tools/config_bench.py cfg2@16384 cfg4 cfg4visc cfg4cfl cfg4full cfg5 ts6 ts36 l96x1@256 l96x64@256 l96x1024@64 l96x8192@8 > gpurun_out/configs_final.jsonl"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
