@@ -145,3 +145,25 @@ def test_overlapped_sample_copy(dev, case, monkeypatch):
     a = _run(op, y, gamma, False, u0, "samples", False, skw, **kw)
     assert a[0].dtype == np.float64 and a[0].shape == b[0].shape
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("case", ["l96", "l63_hi", "linear1", "burgers", "ts6_hi"])
+def test_launch_length_does_not_change_the_chains(dev, case, monkeypatch):
+    """The sampler splits burn-in and sample intervals into launches of at most
+    sampler.STEPS_PER_LAUNCH steps (16 384 by default, so most runs are one
+    launch per block): with the cap forced to 7 -- burn-in, intervals and the
+    in-launch sample blocks all split, speculative rounds cut at every launch
+    boundary -- samples, accept counts and the final state are the same bits."""
+    from ip_mcmc_amd import sampler as S
+
+    rng = np.random.default_rng(12)
+    op, y, gamma, n, skw = _case(case, rng)
+    n = min(n, 64)
+    u0 = 0.1 * rng.normal(size=(n, op.k)) if n > 1 else 0.1 * rng.normal(size=op.k)
+    kw = dict(n_samples=9, burn_in=50, sample_interval=20)
+    a = _run(op, y, gamma, False, u0, "samples", False, skw, **kw)
+    monkeypatch.setattr(S, "STEPS_PER_LAUNCH", 7)
+    b = _run(op, y, gamma, False, u0, "samples", False, skw, **kw)
+    assert a[0].shape == b[0].shape
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert np.asarray(a[1]).sum() > 0
