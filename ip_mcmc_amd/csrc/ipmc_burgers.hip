@@ -580,6 +580,9 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
     T vf[3];
     slot_v(rd.win >= 0 ? rd.win : 0, vf);
     if (s.sum_u || s.sample_every > 0) {
+      const bool sums = s.sum_u && r == 0;
+      RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
+                        sums ? 3 : 0);
       for (int q = 0; q < rd.used; ++q) {
         const int la = spec_last_acc(rd, amode, q);
         T vq[3];
@@ -587,11 +590,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
         if (r == 0) {
           if (s.sum_u) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              const double ud = la >= 0 ? (double)vq[j] : (double)ur[j];
-              s.sum_u[chain * 3 + j] += ud;
-              if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
-            }
+            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
           }
           if (s.sample_every > 0 && clk.next == st + q) {
             // the state after step st+q is a sample
@@ -602,6 +601,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
           }
         }
       }
+      if (sums) rsum.store();
     }
     if (G > 64) __syncthreads();  // bmask / vpk are rewritten next round
     if (rd.win >= 0) {

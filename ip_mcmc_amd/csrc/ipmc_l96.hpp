@@ -207,14 +207,10 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
       }
     }
     if (s.sum_u) {
-      double* su = s.sum_u + chain * D + c0;
-      double* su2 = s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr;
+      RoundSums<M> rsum(s.sum_u + chain * D + c0, s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr, M);
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const double ud = (double)u[j];
-        su[j] += ud;
-        if (su2) su2[j] += ud * ud;
-      }
+      for (int j = 0; j < M; ++j) rsum.add(j, (double)u[j]);
+      rsum.store();
     }
     const int64_t sl = sample_slot(s, st);
     if (sl >= 0) {
@@ -380,17 +376,13 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
     }
     const int lane0 = t - r + sub;  // slot 0's lane for my components
     if (s.sum_u && slot == 0) {
-      double* su = s.sum_u + chain * D + c0;
-      double* su2 = s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr;
+      RoundSums<M> rsum(s.sum_u + chain * D + c0, s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr, M);
       for (int q = 0; q < rd.used; ++q) {
         const int la = spec_last_acc(rd, amode, q);
 #pragma unroll
-        for (int j = 0; j < M; ++j) {
-          const double ud = la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j];
-          su[j] += ud;
-          if (su2) su2[j] += ud * ud;
-        }
+        for (int j = 0; j < M; ++j) rsum.add(j, la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j]);
       }
+      rsum.store();
     }
     if (s.sample_every > 0 && slot == 0) {
       // the samples among the `used` steps: the state after step st+q

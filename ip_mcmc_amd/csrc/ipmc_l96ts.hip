@@ -578,9 +578,12 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
     const T phf = __shfl(phv, wl, 64);
+    const bool sums = s.sum_u && r == 0;
     if ((s.sum_u || s.sample_every > 0) && amode) {
       // recorded states of an accept-mode round: slot q's proposal for q < nar,
       // gathered by every lane (uniform loop), written by lane r == 0
+      RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
+                        sums ? 3 : 0);
       for (int q = 0; q < rd.used; ++q) {
         const int la = spec_last_acc(rd, amode, q);
         T vq[3];
@@ -589,11 +592,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
         if (r == 0) {
           if (s.sum_u) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-              const double ud = la >= 0 ? (double)vq[j] : (double)ur[j];
-              s.sum_u[chain * 3 + j] += ud;
-              if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
-            }
+            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
           }
           if (s.sample_every > 0 && clk.next == st + q) {
             const int64_t sl = clk.take(clk.next);
@@ -603,16 +602,15 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
           }
         }
       }
+      if (sums) rsum.store();
     } else {
-      if (s.sum_u && r == 0) {
+      if (sums) {
+        RoundSums<3> rsum(s.sum_u + chain * 3, s.sum_u2 ? s.sum_u2 + chain * 3 : nullptr, 3);
         for (int qq = 0; qq < rd.used; ++qq) {
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const double ud = (qq == rd.first) ? (double)vf[j] : (double)ur[j];
-            s.sum_u[chain * 3 + j] += ud;
-            if (s.sum_u2) s.sum_u2[chain * 3 + j] += ud * ud;
-          }
+          for (int j = 0; j < 3; ++j) rsum.add(j, (qq == rd.first) ? (double)vf[j] : (double)ur[j]);
         }
+        rsum.store();
       }
       if (s.sample_every > 0 && r == 0) {
         // the samples among the `used` steps: the state after step st+qq

@@ -479,17 +479,14 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
     auto last_acc = [&](int q) { return amode ? (q < nar ? q : nar - 1) : (q == first ? first : -1); };
     if (s.sum_u && sub == 0) {
       // the states after each of the `used` steps, in step order
+      RoundSums<kSpecKMax> rsum(s.sum_u + chain * k, s.sum_u2 ? s.sum_u2 + chain * k : nullptr, k);
       for (int q = 0; q < used; ++q) {
         const int la = last_acc(q);
 #pragma unroll
-        for (int j = 0; j < kSpecKMax; ++j) {
-          if (j < k) {
-            const double ud = la >= 0 ? (double)vgroup[j * kSpecBlock + la] : (double)ur[j];
-            s.sum_u[chain * k + j] += ud;
-            if (s.sum_u2) s.sum_u2[chain * k + j] += ud * ud;
-          }
-        }
+        for (int j = 0; j < kSpecKMax; ++j)
+          if (j < k) rsum.add(j, la >= 0 ? (double)vgroup[j * kSpecBlock + la] : (double)ur[j]);
       }
+      rsum.store();
     }
     if (s.sample_every > 0 && sub == 0) {
       // the samples among the `used` steps: the state after step st+q

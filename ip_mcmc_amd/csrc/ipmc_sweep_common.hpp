@@ -253,6 +253,42 @@ __device__ __forceinline__ int spec_last_acc(const SpecRound& r, bool amode, int
   return amode ? (q < r.nar ? q : r.nar - 1) : (q == r.first ? r.first : -1);
 }
 
+// Running sums Σu, Σu² (ipmc_sweep.sum_u / sum_u2) of a lane's n <= N
+// components over the steps a round (or a step) settles, held in registers
+// meanwhile: one batched load before and one store after.  A `+=` on global
+// memory per step and component compiles to a dependent load / add / store
+// chain -- 2n memory round trips per settled step, as long as the forward map
+// itself for a short one (Lorenz-63: config 2 through MCMCSampler.run with
+// keep="moments").  The additions are the per-step ones in step order: the
+// same bits.
+template <int N>
+struct RoundSums {
+  double a[N], b[N];
+  double* su;
+  double* su2;
+  int n;
+  __device__ __forceinline__ RoundSums(double* su_, double* su2_, int n_) : su(su_), su2(su2_), n(n_) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      a[j] = j < n ? su[j] : 0.0;
+      b[j] = (su2 && j < n) ? su2[j] : 0.0;
+    }
+  }
+  __device__ __forceinline__ void add(int j, double ud) {
+    a[j] = a[j] + ud;
+    b[j] = b[j] + ud * ud;
+  }
+  __device__ __forceinline__ void store() {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      if (j < n) {
+        su[j] = a[j];
+        if (su2) su2[j] = b[j];
+      }
+    }
+  }
+};
+
 // accept iff Φ(u) − Φ(v) > log r   ⇔ exp(Φ(u) − Φ(v)) > r   (accepter.py:62, 121-122)
 template <typename T>
 __device__ __forceinline__ bool pcn_accept(T phu, T phv, uint64_t seed, uint64_t gid, uint64_t step) {

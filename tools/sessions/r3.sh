@@ -226,5 +226,11 @@ case "$1" in
     tools/gpu_session.sh \
       "configs:600:python tools/config_bench.py cfg2@16384 cfg4 cfg4visc cfg4cfl cfg4full cfg5 ts6 ts36 l96x1@256 l96x64@256 l96x1024@64 l96x8192@8 > gpurun_out/configs_final.jsonl"
     ;;
+  rs)  # round sums in registers: the suite, run() moments on config 2, tolerance z's
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q -s" \
+      "example:300:python examples/lorenz63_config2.py > gpurun_out/example_lorenz63_config2.jsonl" \
+      "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_rs.jsonl"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
