@@ -510,17 +510,18 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
         ++nb;
       }
     }
-    if (s.sum_u) {
+    if (s.sum_u) {  // chain a's sums, then chain b's (RoundSums: batched loads and stores)
+      {
+        RoundSums<M> rsum(s.sum_u + ca * D + c0, s.sum_u2 ? s.sum_u2 + ca * D + c0 : nullptr, M);
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const double a = (double)ua[j];
-        s.sum_u[ca * D + c0 + j] += a;
-        if (s.sum_u2) s.sum_u2[ca * D + c0 + j] += a * a;
-        if (has_b) {
-          const double b = (double)ub[j];
-          s.sum_u[cb * D + c0 + j] += b;
-          if (s.sum_u2) s.sum_u2[cb * D + c0 + j] += b * b;
-        }
+        for (int j = 0; j < M; ++j) rsum.add(j, (double)ua[j]);
+        rsum.store();
+      }
+      if (has_b) {
+        RoundSums<M> rsum(s.sum_u + cb * D + c0, s.sum_u2 ? s.sum_u2 + cb * D + c0 : nullptr, M);
+#pragma unroll
+        for (int j = 0; j < M; ++j) rsum.add(j, (double)ub[j]);
+        rsum.store();
       }
     }
     const int64_t sl = sample_slot(s, st);

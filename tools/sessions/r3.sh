@@ -232,5 +232,11 @@ case "$1" in
       "example:300:python examples/lorenz63_config2.py > gpurun_out/example_lorenz63_config2.jsonl" \
       "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_rs.jsonl"
     ;;
+  fin)  # final tree: the suite, smoke, e2e, then the published line and its same-box profiles (session c)
+    tools/gpu_session.sh \
+      "pytest_gpu:900:$PYT tests -m gpu -q -s" \
+      "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" \
+      "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_final.jsonl" && tools/sessions/r3.sh c
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
