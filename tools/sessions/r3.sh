@@ -238,5 +238,9 @@ case "$1" in
       "smoke:200:python -c 'import __graft_entry__ as g; g.smoke()'" \
       "e2e:300:python tools/sampler_e2e.py 65536 20 1 > gpurun_out/e2e_final.jsonl" && tools/sessions/r3.sh c
     ;;
+  ex)  # the reference studies on the final tree
+    tools/gpu_session.sh \
+      "examples:500:python examples/lorenz_thesis.py > gpurun_out/example_lorenz_thesis.json && python examples/burgers_beta.py > gpurun_out/example_burgers_beta.jsonl && python examples/stuart_examples.py > gpurun_out/example_stuart.jsonl && python examples/stuart_reference.py > gpurun_out/stuart_reference.jsonl"
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
