@@ -4,7 +4,9 @@ CountedAccepter(pCNAccepter(EvolutionPotential(G, data, noise))), one numpy
 Generator for the data and the sampler, one chain, n_samples = 5 000 with the
 default burn-in 1 000 and interval 200 -- BASELINE config 1's "1 chain on the
 NumPy path".  The Python G runs in MCMCSampler's host-side step
-(ip_mcmc_amd/hostloop.py); the draws come from the GPU.  Instead of the
+(ip_mcmc_amd/hostloop.py); the draws come from the GPU when there is one and
+from libipmc_host.so (the kernels' draw arithmetic compiled for the CPU, the
+same bits) when there is none.  Instead of the
 reference's histogram this prints the sample mean and variance next to the
 exact posterior (results.org:59-62) and the wall time.
 

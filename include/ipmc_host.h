@@ -1,0 +1,64 @@
+/* ipmc_host.h — the counter-based draws of the pCN path on the host CPU.
+ *
+ * libipmc_host.so (ip_mcmc_amd/lib/) is compiled by g++ from the same source
+ * as the device draws (ip_mcmc_amd/csrc/ipmc_rng.hpp: Philox4x32-10,
+ * Box–Muller with the deterministic log / sincos, the proposal-noise element),
+ * so every value below is bit-identical to its libipmc.so twin.  It needs no
+ * GPU and no HIP runtime: it is the randomness of MCMCSampler.run's host step
+ * on a machine without a GPU (BASELINE config 1, "1 chain on NumPy CPU path").
+ *
+ * Reference interface each entry point replaces (ip_mcmc, report/code.org:12-13:
+ * one numpy Generator threaded through the sampler):
+ *   ipmc_host_pcn_draws  GaussianDistribution.sample -> rng.multivariate_normal
+ *                        (distribution.py:114-118) for the proposal w of
+ *                        ConstSteppCNProposer.__call__ (proposer.py:78-82), and
+ *                        log of rng.random() (accepter.py:62) -- a block of steps
+ *                        at once; twin of ipmc_pcn_draws (ipmc.h)
+ *   ipmc_host_normal     rng.multivariate_normal's standard normals; twin of
+ *                        ipmc_normal
+ *   ipmc_host_uniform    rng.random() (accepter.py:62); twin of ipmc_uniform
+ *   ipmc_host_step_uniforms  further rng.random() calls within one step
+ *
+ * Host pointers only.  Returns IPMC_OK (0) or an IPMC_ERR_* code of ipmc.h;
+ * ipmc_host_last_error() gives the message (thread-local).
+ */
+#ifndef IPMC_HOST_H
+#define IPMC_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPMC_HOST_ABI_VERSION 1
+
+int ipmc_host_abi_version(void);
+const char* ipmc_host_last_error(void);
+
+/* w[s][c][j] (dtype IPMC_F32 / IPMC_F64, [n_steps, n_chains, k] row-major) =
+ * the proposal noise of global chain chain_offset + c at pCN step step0 + s:
+ * prior_sqrt[j]·ξ_j (diagonal prior) or Σ_{i<=j} prior_chol[j][i]·ξ_i;
+ * log_r[s][c] (f64, may be NULL) = log of the accept uniform.  n_threads
+ * <= 0: the host's hardware threads (large blocks only). */
+int ipmc_host_pcn_draws(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step0, int64_t n_steps,
+                        int32_t k, int32_t dtype, const void* prior_sqrt, const void* prior_chol, void* w,
+                        double* log_r, int32_t n_threads);
+
+/* out[c][j] = ξ_j of global chain chain_offset + c at `step` (dtype f32/f64). */
+int ipmc_host_normal(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, int32_t k,
+                     int32_t dtype, void* out);
+
+/* out[c] = the accept uniform r in [0, 1) of global chain chain_offset + c at `step`. */
+int ipmc_host_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uint64_t step, double* out);
+
+/* out[i] (i < n) = the i-th uniform of one (chain, step): i = 0 is the accept
+ * uniform (slot 0xFFFFFFFF), i > 0 slot 0xFFFFFFFF - i -- the extra uniforms
+ * a caller's own accepter may draw in a step (MCMCSampler's generic host tier). */
+int ipmc_host_step_uniforms(uint64_t seed, int64_t chain, uint64_t step, int32_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IPMC_HOST_H */

@@ -327,8 +327,9 @@ __global__ void reg_add_kernel(int64_t n, int k, const T* __restrict__ u, const 
 }
 
 // ipmc_pcn_draws: one thread per (step, chain, component), grid-stride.  w is
-// formed with pcn_propose's / chol_propose's operations (the same bits as the
-// sweep kernels' proposal noise); the j = 0 thread also writes log r.
+// formed with pcn_propose's / chol_propose's operations (draw_w, ipmc_rng.hpp:
+// the same bits as the sweep kernels' proposal noise and as the host
+// library's ipmc_host_pcn_draws); the j = 0 thread also writes log r.
 template <typename T>
 __global__ void draws_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t step0, int64_t total, int k,
                              const T* __restrict__ sq, const T* __restrict__ chol, T* __restrict__ w,
@@ -340,20 +341,7 @@ __global__ void draws_kernel(uint64_t seed, int64_t c_off, int64_t n, uint64_t s
     const int64_t s = sc / n;
     const uint64_t gid = (uint64_t)(c_off + (sc - s * n));
     const uint64_t step = step0 + (uint64_t)s;
-    double z0, z1;
-    T wj;
-    if (chol) {
-      wj = (T)0;
-      for (int ii = 0; ii <= j; ii += 2) {
-        normal_pair(seed, gid, step, (uint32_t)(ii >> 1), z0, z1);
-        wj = wj + (T)z0 * chol[(int64_t)j * k + ii];
-        if (ii + 1 <= j) wj = wj + (T)z1 * chol[(int64_t)j * k + ii + 1];
-      }
-    } else {
-      normal_pair(seed, gid, step, (uint32_t)(j >> 1), z0, z1);
-      wj = sq[j] * (T)((j & 1) ? z1 : z0);
-    }
-    w[i] = wj;
+    w[i] = draw_w<T>(seed, gid, step, j, k, sq, chol);
     if (j == 0 && log_r) log_r[sc] = det_log(accept_uniform(seed, gid, step));
   }
 }

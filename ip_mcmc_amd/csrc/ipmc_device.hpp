@@ -1,11 +1,7 @@
 // Device building blocks for the pCN sweep kernels (gfx950 / CDNA4).
 //
-//  * Philox4x32-10 counter-based RNG: ctr = (slot, chain, step_lo, step_hi),
-//    key = (seed_lo, seed_hi). slot j -> normal pair (2j, 2j+1) of the
-//    proposal (proposer.py:81-82's w ~ N(0, C)), slot 0xFFFFFFFF -> the accept
-//    uniform (accepter.py:62's rng.random()).
-//  * Deterministic log / sincos(2*pi*t) built from + - * / in a fixed order,
-//    so every draw is bit-identical to the CPU oracle.
+//  * the counter-based draws (Philox4x32-10, deterministic log / sincos,
+//    Box–Muller) come from ipmc_rng.hpp, compiled for host and device.
 //  * Cross-lane halo exchange for chains spread over 2/4 lanes (DPP quad_perm,
 //    no LDS traffic) or 8/16 lanes (ds_bpermute).
 #pragma once
@@ -13,132 +9,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ipmc_rng.hpp"
+
 namespace ipmc {
 
 // LDS per CU on gfx950 (MI355X): the static LDS of any block must fit this.
 constexpr size_t kLdsBytesPerCU = 160 * 1024;
 
-// ---------------------------------------------------------------- Philox
-struct u32x4 {
-  uint32_t x, y, z, w;
-};
-
-__device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                               uint32_t k0, uint32_t k1) {
-  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r > 0) {
-      k0 += W0;
-      k1 += W1;
-    }
-    const uint32_t lo0 = M0 * c0, hi0 = __umulhi(M0, c0);
-    const uint32_t lo1 = M1 * c2, hi1 = __umulhi(M1, c2);
-    const uint32_t n0 = hi1 ^ c1 ^ k0;
-    const uint32_t n2 = hi0 ^ c3 ^ k1;
-    c0 = n0;
-    c1 = lo1;
-    c2 = n2;
-    c3 = lo0;
-  }
-  return {c0, c1, c2, c3};
-}
-
-__device__ __forceinline__ u32x4 philox_draw(uint64_t seed, uint64_t chain, uint64_t step, uint32_t slot) {
-  return philox4x32_10(slot, (uint32_t)chain, (uint32_t)step, (uint32_t)(step >> 32), (uint32_t)seed,
-                       (uint32_t)(seed >> 32));
-}
-
-// ------------------------------------------------------ deterministic math
-// Bit-identical to oracle/orc_rng.c (same constants, same operation order;
-// compiled with -ffp-contract=off so no operation is fused).
-__device__ __forceinline__ double det_log(double x) {
-  if (x == 0.0) return -__builtin_inf();
-  const uint64_t b = (uint64_t)__double_as_longlong(x);
-  int e = (int)((b >> 52) & 0x7ff) - 1023;
-  double m = __longlong_as_double((long long)((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
-  if (m > 0x1.6a09e667f3bcdp+0) {
-    m = m * 0.5;
-    e = e + 1;
-  }
-  const double f = m - 1.0;
-  const double s = f / (2.0 + f);
-  const double z = s * s;
-  double p = 0x1.642c8590b2164p-5;
-  p = p * z + 0x1.8618618618618p-5;
-  p = p * z + 0x1.af286bca1af28p-5;
-  p = p * z + 0x1.e1e1e1e1e1e1ep-5;
-  p = p * z + 0x1.1111111111111p-4;
-  p = p * z + 0x1.3b13b13b13b14p-4;
-  p = p * z + 0x1.745d1745d1746p-4;
-  p = p * z + 0x1.c71c71c71c71cp-4;
-  p = p * z + 0x1.2492492492492p-3;
-  p = p * z + 0x1.999999999999ap-3;
-  p = p * z + 0x1.5555555555555p-2;
-  const double s2 = s + s;
-  const double lm = s2 + s2 * (z * p);
-  const double de = (double)e;
-  return de * 0x1.62e42fee00000p-1 + (de * 0x1.a39ef35793c76p-33 + lm);
-}
-
-__device__ __forceinline__ void det_sincos_2pi(double t, double& so, double& co) {
-  const double y = t * 4.0;
-  int qi = (int)y;
-  double r = y - (double)qi;
-  if (r > 0.5) {
-    r = r - 1.0;
-    qi = qi + 1;
-  }
-  const double phi = r * 0x1.921fb54442d18p+0;
-  const double z = phi * phi;
-  double ps = 0x1.952c77030ad4ap-49;
-  ps = ps * z + -0x1.ae7f3e733b81fp-41;
-  ps = ps * z + 0x1.6124613a86d09p-33;
-  ps = ps * z + -0x1.ae64567f544e4p-26;
-  ps = ps * z + 0x1.71de3a556c734p-19;
-  ps = ps * z + -0x1.a01a01a01a01ap-13;
-  ps = ps * z + 0x1.1111111111111p-7;
-  ps = ps * z + -0x1.5555555555555p-3;
-  const double sv = phi + phi * (z * ps);
-  double pc = -0x1.6827863b97d97p-53;
-  pc = pc * z + 0x1.ae7f3e733b81fp-45;
-  pc = pc * z + -0x1.93974a8c07c9dp-37;
-  pc = pc * z + 0x1.1eed8eff8d898p-29;
-  pc = pc * z + -0x1.27e4fb7789f5cp-22;
-  pc = pc * z + 0x1.a01a01a01a01ap-16;
-  pc = pc * z + -0x1.6c16c16c16c17p-10;
-  pc = pc * z + 0x1.5555555555555p-5;
-  pc = pc * z + -0x1.0000000000000p-1;
-  const double cv = 1.0 + z * pc;
-  switch (qi & 3) {
-    case 0: so = sv;  co = cv;  break;
-    case 1: so = cv;  co = -sv; break;
-    case 2: so = -sv; co = -cv; break;
-    default: so = -cv; co = sv; break;
-  }
-}
-
-// Box–Muller pair for components (2*slot, 2*slot+1).
-__device__ __forceinline__ void normal_pair(uint64_t seed, uint64_t chain, uint64_t step, uint32_t slot,
-                                            double& z0, double& z1) {
-  const u32x4 o = philox_draw(seed, chain, step, slot);
-  const uint64_t a = ((((uint64_t)o.x << 32) | o.y) >> 11) + 1;
-  const uint64_t b = (((uint64_t)o.z << 32) | o.w) >> 11;
-  const double u1 = (double)a * 0x1.0p-53;
-  const double u2 = (double)b * 0x1.0p-53;
-  const double rad = __builtin_sqrt(-2.0 * det_log(u1));
-  double sv, cv;
-  det_sincos_2pi(u2, sv, cv);
-  z0 = rad * cv;
-  z1 = rad * sv;
-}
-
-__device__ __forceinline__ double accept_uniform(uint64_t seed, uint64_t chain, uint64_t step) {
-  const u32x4 o = philox_draw(seed, chain, step, 0xFFFFFFFFu);
-  const uint64_t a = (((uint64_t)o.x << 32) | o.y) >> 11;
-  return (double)a * 0x1.0p-53;
-}
+// Philox draws, deterministic log / sincos, Box–Muller and the proposal
+// noise element: ipmc_rng.hpp (shared with the host library).
 
 // ------------------------------------------------------------- arithmetic
 // madd<FMA>(a, b, c) = c + a*b, fused (one rounding) or not (two roundings).

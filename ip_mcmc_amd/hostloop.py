@@ -77,9 +77,49 @@ def device_raw_draws(seed, chain_offset, n_chains, step0, n_steps, k, device=Non
     return xi.cpu().numpy(), r.cpu().numpy()
 
 
-# the providers the loop uses (tests on a CPU-only machine substitute the
-# oracle's draws for these; the product path has no other source)
-DRAWS = {"w": device_draws, "raw": device_raw_draws}
+def host_draws(seed, chain_offset, n_chains, step0, n_steps, k, np_dtype, prior_sqrt, prior_chol, device=None):
+    """The same (w, log r) from libipmc_host.so (ipmc_host_pcn_draws): the
+    kernels' draw arithmetic compiled for the host CPU (csrc/ipmc_rng.hpp)."""
+    from . import _hostlib
+
+    return _hostlib.pcn_draws(seed, chain_offset, n_chains, step0, n_steps, k, np_dtype, prior_sqrt, prior_chol)
+
+
+def host_raw_draws(seed, chain_offset, n_chains, step0, n_steps, k, device=None):
+    """The same (ξ, r) from libipmc_host.so (ipmc_host_normal / ipmc_host_uniform)."""
+    from . import _hostlib
+
+    xi = np.empty((n_steps, n_chains, k), dtype=np.float64)
+    r = np.empty((n_steps, n_chains), dtype=np.float64)
+    for s in range(n_steps):
+        xi[s] = _hostlib.normals(seed, chain_offset, n_chains, step0 + s, k)
+        r[s] = _hostlib.uniforms(seed, chain_offset, n_chains, step0 + s)
+    return xi, r
+
+
+# Where the host step's draws come from: "device" (ipmc_pcn_draws on the GPU),
+# "host" (libipmc_host.so, the same bits on the CPU) or "auto" (the GPU when
+# torch sees one, else the host library -- BASELINE config 1 on a machine
+# without a GPU).
+DRAW_SOURCE = "auto"
+
+
+def draw_source():
+    if DRAW_SOURCE != "auto":
+        return DRAW_SOURCE
+    return "device" if torch.cuda.is_available() else "host"
+
+
+def _auto_w(*a, **kw):
+    return (device_draws if draw_source() == "device" else host_draws)(*a, **kw)
+
+
+def _auto_raw(*a, **kw):
+    return (device_raw_draws if draw_source() == "device" else host_raw_draws)(*a, **kw)
+
+
+# the providers the loop uses (tests may substitute others)
+DRAWS = {"w": _auto_w, "raw": _auto_raw}
 # run_structured's one-chain f64 loop on Python floats (tests switch it off to
 # compare it with the array loop)
 SINGLE_CHAIN_FLOATS = True
@@ -373,36 +413,112 @@ def initial_phi(plan, U, device):
 class StepRNG:
     """The rng handed to a caller's proposer/accepter in the generic tier: the
     draws of one (chain, step), like the reference's MockRNG seam
-    (test_utilities.py:11-26).  multivariate_normal(mean, cov) = mean + sqrt(C)·ξ
-    (diagonal C) or mean + L·ξ in the kernels' order; random() = r."""
+    (test_utilities.py:11-26).
 
-    def __init__(self):
-        self.xi = None
-        self.r = None
+    Normals come from the step's Philox stream in component order through a
+    cursor: the first ``multivariate_normal(mean, cov)`` of a step returns
+    mean + sqrt(C)·ξ[0:k] (diagonal C) or mean + L·ξ[0:k] in the kernels'
+    order -- the structured tier's and the kernels' proposal -- and a second
+    draw in the same step continues with ξ[k:2k] (e.g. a product prior that
+    samples its components one by one, distribution.py:57-59).  Uniforms
+    likewise: the first ``random()`` is the accept uniform r (Philox slot
+    0xFFFFFFFF), further ones come from slots 0xFFFFFFFE, 0xFFFFFFFD, ...  Draws
+    beyond the pre-drawn block come from libipmc_host.so (the same bits).
+    ``standard_normal``, ``normal``, ``uniform`` and ``lognormal`` use the same
+    cursors; any other Generator method raises AttributeError."""
 
-    def set(self, xi, r):
-        self.xi, self.r = xi, r
+    SUPPORTED = ("multivariate_normal", "random", "standard_normal", "normal", "uniform", "lognormal")
 
-    def multivariate_normal(self, mean=None, cov=None):
+    def __init__(self, seed=0):
+        self.seed = int(seed)
+        self.gid = self.step = 0
+        self.xi = np.zeros(0)
+        self.r = 0.0
+        self._n = self._u = 0
+
+    def set(self, xi, r, gid=0, step=0):
+        self.xi, self.r = np.asarray(xi, dtype=np.float64), float(r)
+        self.gid, self.step = int(gid), int(step)
+        self._n = self._u = 0
+
+    def __getattr__(self, name):
+        raise AttributeError(f"the generic tier's rng supports {', '.join(self.SUPPORTED)}; "
+                             f"numpy Generator.{name} has no counter-based twin here")
+
+    # ------------------------------------------------------------ cursors
+    def _normals(self, m):
+        j0, j1 = self._n, self._n + m
+        self._n = j1
+        if j1 <= self.xi.shape[0]:
+            return self.xi[j0:j1].copy()
+        from . import _hostlib
+
+        return _hostlib.normals(self.seed, self.gid, 1, self.step, j1)[0, j0:j1]
+
+    def _uniforms(self, m):
+        i0, i1 = self._u, self._u + m
+        self._u = i1
+        out = np.empty(m)
+        extra = None
+        for i in range(i0, i1):
+            if i == 0:
+                out[i - i0] = self.r
+            else:
+                if extra is None:
+                    from . import _hostlib
+
+                    extra = _hostlib.extra_uniforms(self.seed, self.gid, self.step, i1)
+                out[i - i0] = extra[i]
+        return out
+
+    @staticmethod
+    def _count(size):
+        if size is None:
+            return 1
+        return int(np.prod(np.atleast_1d(size)))
+
+    @staticmethod
+    def _shape(v, size):
+        return float(v[0]) if size is None else v.reshape(size)
+
+    # --------------------------------------------------- Generator methods
+    def multivariate_normal(self, mean=None, cov=None, size=None):
         mean = np.atleast_1d(np.asarray(mean, dtype=np.float64))
         k = mean.shape[0]
-        if k > self.xi.shape[0]:
-            raise ValueError(f"draw of dimension {k} > the chain's {self.xi.shape[0]}")
-        xi = self.xi[:k]
         cov = np.asarray(cov, dtype=np.float64).reshape(k, k)
-        if np.all(cov == np.diag(np.diag(cov))):
-            return np.sqrt(np.diag(cov)) * xi + mean
-        L = np.linalg.cholesky(cov)
-        w = np.zeros(k)
-        for j in range(k):
-            a = 0.0
-            for i in range(j + 1):
-                a = a + float(xi[i]) * float(L[j, i])
-            w[j] = a
-        return w + mean
+        diag = bool(np.all(cov == np.diag(np.diag(cov))))
+        L = None if diag else np.linalg.cholesky(cov)
+        rows = []
+        for _ in range(self._count(size)):
+            xi = self._normals(k)
+            if diag:
+                rows.append(np.sqrt(np.diag(cov)) * xi + mean)
+                continue
+            w = np.zeros(k)
+            for j in range(k):
+                a = 0.0
+                for i in range(j + 1):
+                    a = a + float(xi[i]) * float(L[j, i])
+                w[j] = a
+            rows.append(w + mean)
+        if size is None:
+            return rows[0]
+        return np.stack(rows).reshape(tuple(np.atleast_1d(size)) + (k,))
 
-    def random(self):
-        return float(self.r)
+    def random(self, size=None):
+        return self._shape(self._uniforms(self._count(size)), size)
+
+    def standard_normal(self, size=None):
+        return self._shape(self._normals(self._count(size)), size)
+
+    def normal(self, loc=0.0, scale=1.0, size=None):
+        return self._shape(loc + scale * self._normals(self._count(size)), size)
+
+    def uniform(self, low=0.0, high=1.0, size=None):
+        return self._shape(low + (high - low) * self._uniforms(self._count(size)), size)
+
+    def lognormal(self, mean=0.0, sigma=1.0, size=None):
+        return self._shape(np.exp(mean + sigma * self._normals(self._count(size))), size)
 
 
 def _counted(acc):
@@ -420,12 +536,19 @@ def _counted(acc):
 def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_samples, interval, rec, device,
                 verbose=False):
     """The reference's _step (sampler.py:35-41) per chain with StepRNG draws.
-    Returns per-chain (calls, accepts) of every CountedAccepter found."""
+    Returns (CountedAccepters found, their per-chain (calls, accepts), steps
+    run, per-chain accept decisions).
+
+    A stateful proposer (a step counter ``i``, like VarStep*, proposer.py:105)
+    sees every chain's call of one step with the counter the step starts with,
+    and advances once per step, as one chain of the reference would."""
     C_, k = U.shape
     total = n_burn + n_samples * interval
     counted = _counted(accepter)
     per = {id(ca): (np.zeros(C_, dtype=np.int64), np.zeros(C_, dtype=np.int64)) for ca in counted}
-    rng = StepRNG()
+    decided = np.zeros(C_, dtype=np.int64)
+    rng = StepRNG(seed)
+    stateful = hasattr(proposer, "i")
     block = max(1, min(total, DRAW_BLOCK_BYTES // max(1, C_ * k * 8)))
     u_rows = [np.asarray(U[c], dtype=np.float64).copy() for c in range(C_)]
     done = 0
@@ -435,15 +558,24 @@ def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_sampl
         xi, r = DRAWS["raw"](seed, chain_offset, C_, step + done, nb, k, device)
         for s in range(nb):
             _announce(verbose, done + s, n_burn, interval, n_samples)
+            i_step = proposer.i if stateful else None
+            i_next = i_step
             for c in range(C_):
                 before = [(ca.calls, ca.accepts) for ca in counted]
-                rng.set(xi[s, c], r[s, c])
+                rng.set(xi[s, c], r[s, c], chain_offset + c, step + done + s)
+                if stateful:
+                    proposer.i = i_step
                 v = proposer(u_rows[c], rng)
+                if stateful:
+                    i_next = proposer.i
                 if accepter(u_rows[c], v, rng):
                     u_rows[c] = np.asarray(v, dtype=np.float64)
+                    decided[c] += 1
                 for ca, (c0, a0) in zip(counted, before):
                     per[id(ca)][0][c] += int(np.sum(ca.calls)) - int(np.sum(c0))
                     per[id(ca)][1][c] += int(np.sum(ca.accepts)) - int(np.sum(a0))
+            if stateful:
+                proposer.i = i_next
             if done + s >= n_burn:
                 Ucur = np.stack(u_rows)
                 rec.accumulate(Ucur)
@@ -452,7 +584,7 @@ def run_generic(proposer, accepter, U, seed, chain_offset, step, n_burn, n_sampl
                     rec.record(post // interval - 1, Ucur)
         done += nb
     U[:] = np.stack(u_rows).astype(U.dtype) if C_ else U
-    return counted, per, total
+    return counted, per, total, decided
 
 
 # --------------------------------------------------------------------- run
@@ -488,10 +620,11 @@ def run(sampler, u_0, n_samples, burn_in, sample_interval, keep, sample_file, re
         plan = HostPlan(sampler.proposer, sampler.accepter, k)
     except GenericComposition:
         plan = None
-    accept_kind = None if plan is None else plan.accept_kind
+    # a generic run caches no accept potential (its Φ is NaN): "generic" tells a
+    # later structured or device run to recompute Φ(u) instead of reusing it
+    accept_kind = "generic" if plan is None else plan.accept_kind
     if resume:
-        if accept_kind is not None:
-            _check_resume(u_0, sampler.chain_offset, accept_kind)
+        _check_resume(u_0, sampler.chain_offset, accept_kind)
         rng.seed, rng.step = u_0.seed, u_0.step
         if hasattr(sampler.proposer, "i"):
             sampler.proposer.i = u_0.proposer_i
@@ -511,7 +644,8 @@ def run(sampler, u_0, n_samples, burn_in, sample_interval, keep, sample_file, re
     # reference's loop runs no step between its records, sampler.py:23-28)
     n_rec = n_samples if sample_interval > 0 else 0
     if plan is not None:
-        if resume and u_0.dtype == state_dtype and u_0.phi.shape[0] == n_chains:
+        if (resume and u_0.dtype == state_dtype and u_0.phi.shape[0] == n_chains
+                and u_0.accept_kind != "generic"):
             phi = np.array(u_0.phi, dtype=T)
         else:
             phi = initial_phi(plan, U, device)
@@ -532,9 +666,9 @@ def run(sampler, u_0, n_samples, burn_in, sample_interval, keep, sample_file, re
         phi = np.full(n_chains, np.nan, dtype=T)
         counted = _counted(sampler.accepter)
         prev = [(ca.calls, ca.accepts) for ca in counted]
-        counted, per, total = run_generic(sampler.proposer, sampler.accepter, U, rng.seed, sampler.chain_offset,
-                                          rng.step, n_burn, n_rec, eff_interval, rec, device, sampler.verbose)
-        acc_np = per[id(counted[0])][1] if counted else np.zeros(n_chains, dtype=np.int64)
+        counted, per, total, acc_np = run_generic(sampler.proposer, sampler.accepter, U, rng.seed,
+                                                  sampler.chain_offset, rng.step, n_burn, n_rec, eff_interval, rec,
+                                                  device, sampler.verbose)
         for ca, (c0, a0) in zip(counted, prev):
             # per-chain arrays for many chains, ints for one (the device path's convention)
             c, a = per[id(ca)]

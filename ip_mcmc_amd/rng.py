@@ -53,10 +53,13 @@ class PhiloxRNG:
         return dev.uniforms(self.seed, chain_offset, n_chains, self.step if step is None else step, device)
 
     def host_normals(self, k):
-        """k fresh standard normals as a numpy array (drawn on the device)."""
-        z = self.normals(1, k, step=HOST_STEP_BASE + self._host_draws, chain_offset=0)
+        """k fresh standard normals as a numpy array: ipmc_host_normal of
+        libipmc_host.so (the device draws' arithmetic on the CPU; no GPU needed)."""
+        from . import _hostlib
+
+        z = _hostlib.normals(self.seed, 0, 1, HOST_STEP_BASE + self._host_draws, k)
         self._host_draws += 1
-        return z.double().cpu().numpy().reshape(k)
+        return z.reshape(k)
 
 
 # SURVEY §8(b)'s name for the same handle

@@ -259,11 +259,12 @@ class MCMCSampler:
         state_dtype = "float64" if td == torch.float64 else "float32"
         if resume and u_0.phi.shape[0] != n_chains:
             raise ValueError("ChainState phi does not match its u")
-        if resume and u_0.dtype == state_dtype:
+        if resume and u_0.dtype == state_dtype and u_0.accept_kind != "generic":
             phi.copy_(dev.to_device(u_0.phi, td, device))
         else:
-            # a fresh run, or a state saved in the other precision: its Φ cache
-            # is not this dtype's Φ(u), so recompute it
+            # a fresh run, a state saved in the other precision (its Φ cache is
+            # not this dtype's Φ(u)) or by the generic host tier (no Φ cache):
+            # recompute it
             call("ipmc_init_phi", C.byref(model), C.byref(sw), stream)
 
         step = rng.step
@@ -507,13 +508,15 @@ def _check_resume(state, chain_offset, accept_kind):
     """A ChainState continues exactly only on the same Philox streams (global
     chain ids) and the same accept potential (Φ for pCNAccepter, I = Φ + the
     regularizer for StandardRWAccepter); anything else is an error.  States
-    saved before these fields existed carry None and are not checked."""
+    saved before these fields existed carry None and are not checked; states
+    of the generic host tier ("generic") cache no potential, and the resuming
+    run recomputes it."""
     if state.chain_offset is not None and state.chain_offset != chain_offset:
         raise ValueError(
             f"ChainState was saved with chain_offset={state.chain_offset}, the sampler has {chain_offset}: "
             "the chains would continue on other Philox streams"
         )
-    if state.accept_kind is not None and state.accept_kind != accept_kind:
+    if state.accept_kind not in (None, "generic") and accept_kind != "generic" and state.accept_kind != accept_kind:
         raise ValueError(
             f"ChainState caches the {state.accept_kind!r} accept potential, this sampler accepts on "
             f"{accept_kind!r} (pcn = pCNAccepter's Φ, rw_reg = StandardRWAccepter's Φ + regularizer)"

@@ -37,6 +37,35 @@ def test_pcn_draws_match_oracle(dev, orc, dtype, dense):
     assert np.array_equal(lr, lro)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("dense", [False, True])
+def test_host_library_draws_equal_device_draws(dev, dtype, dense):
+    """libipmc_host.so (g++, the CPU) and ipmc_pcn_draws / ipmc_normal /
+    ipmc_uniform (hipcc, the GPU) compile one source (csrc/ipmc_rng.hpp) and
+    give the same bits -- over a large block (threaded on the host), extreme
+    seeds, chain ids near 2^32 and steps near 2^63."""
+    from ip_mcmc_amd import _hostlib, device as D
+    from ip_mcmc_amd.hostloop import device_draws, host_draws
+
+    rng = np.random.default_rng(4)
+    k = 40 if not dense else 9
+    if dense:
+        A = rng.normal(size=(k, k))
+        L, sq = np.linalg.cholesky(A @ A.T + k * np.eye(k)), None
+    else:
+        L, sq = None, rng.uniform(0.5, 2, size=k)
+    for seed, off, C_, step0, n in ((0xBEEF, 0, 4096, 0, 16), (2**64 - 1, 2**32 - 300, 300, 2**63 - 4, 4)):
+        w, lr = device_draws(seed, off, C_, step0, n, k, dtype, sq, L, dev)
+        wh, lrh = host_draws(seed, off, C_, step0, n, k, dtype, sq, L)
+        assert np.array_equal(w, wh) and np.array_equal(lr, lrh)
+    # the raw normals and uniforms, including steps from 2^63 on (host-side draws)
+    for step in (7, 2**63 + 3):
+        z = D.normals(11, 5, 64, step, 13, torch.float64, dev).cpu().numpy()
+        assert np.array_equal(z, _hostlib.normals(11, 5, 64, step, 13))
+        u = D.uniforms(11, 5, 64, step, dev).cpu().numpy()
+        assert np.array_equal(u, _hostlib.uniforms(11, 5, 64, step))
+
+
 def test_python_G_matches_reference_fixture_with_device_draws(dev, golden):
     from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
                              MCMCSampler, PhiloxRNG, pCNAccepter)

@@ -1,10 +1,11 @@
 """The host-side step (ip_mcmc_amd/hostloop.py) on the reference's own fixtures.
 
-On this CPU-only machine the draws come from the oracle's Philox restatement
-(bit-identical to ipmc_pcn_draws, which tests/test_gpu_hostloop.py checks on
-the GPU); everything else is the product code: the composition parsing, the
-proposal arithmetic, Python forward maps and predicates, the accept rule and
-the counters.  The fixtures are the reference sampler's chains with the same
+On this CPU-only machine the draws come from the product's host library
+libipmc_host.so (the kernels' ipmc_rng.hpp compiled by g++; checked against
+the oracle's Philox restatement here and against ipmc_pcn_draws on the GPU by
+tests/test_gpu_hostloop.py), so every test below runs the product path end to
+end: the composition parsing, the draws, the proposal arithmetic, Python
+forward maps and predicates, the accept rule and the counters.  The fixtures are the reference sampler's chains with the same
 draws injected (tests/golden/make_golden.py): config 1's closure
 G(u) = np.dot(g, u) (stuart_examples.py:69-70), a constraint predicate
 (accepter.py:39-55), a non-diagonal prior, and the reference Burgers study's
@@ -20,6 +21,7 @@ from ip_mcmc_amd import hostloop
 
 
 def _oracle_w(orc):
+    """The oracle's restatement of ipmc_pcn_draws (the checker of the host library)."""
     def draws(seed, off, C_, step0, n, k, T, sq, chol, device=None):
         w = np.empty((n, C_, k), dtype=T)
         lr = np.empty((n, C_))
@@ -42,19 +44,47 @@ def _oracle_w(orc):
     return draws
 
 
-def _oracle_raw(orc):
-    def draws(seed, off, C_, step0, n, k, device=None):
-        xi = np.stack([orc.normals(seed, off, C_, step0 + s, k) for s in range(n)])
-        r = np.stack([orc.uniforms(seed, off, C_, step0 + s) for s in range(n)])
-        return xi, r
-
-    return draws
-
-
 @pytest.fixture
-def odraws(orc, monkeypatch):
-    monkeypatch.setitem(hostloop.DRAWS, "w", _oracle_w(orc))
-    monkeypatch.setitem(hostloop.DRAWS, "raw", _oracle_raw(orc))
+def odraws(monkeypatch):
+    """The product's draws on a machine without a GPU: libipmc_host.so."""
+    monkeypatch.setattr(hostloop, "DRAW_SOURCE", "auto")
+    assert hostloop.draw_source() == "host"
+
+
+@pytest.mark.parametrize("T", [np.float64, np.float32])
+def test_host_library_draws_equal_the_oracle(orc, T):
+    """ipmc_host_pcn_draws (diagonal and Cholesky priors, f32/f64) and the raw
+    normals / uniforms equal the oracle's restatement bit for bit."""
+    rng = np.random.default_rng(2)
+    k = 7
+    A = rng.normal(size=(k, k))
+    L = np.linalg.cholesky(A @ A.T + k * np.eye(k))
+    sq = rng.uniform(0.5, 2.0, size=k)
+    for prior_sqrt, chol in ((sq, None), (None, L)):
+        for seed, off, C_, step0, n in ((42, 0, 5, 0, 3), (2**64 - 3, 2**32 - 6, 6, 2**40 + 7, 2)):
+            w, lr = hostloop.host_draws(seed, off, C_, step0, n, k, T, prior_sqrt, chol)
+            wo, lro = _oracle_w(orc)(seed, off, C_, step0, n, k, T, prior_sqrt, chol)
+            assert w.dtype == T and np.array_equal(w, wo) and np.array_equal(lr, lro)
+    xi, r = hostloop.host_raw_draws(9, 3, 4, 100, 2, 5)
+    assert np.array_equal(xi[1], orc.normals(9, 3, 4, 101, 5)) and np.array_equal(r[1], orc.uniforms(9, 3, 4, 101))
+
+
+def test_host_library_threads_and_errors():
+    """A block large enough to be split over threads equals the one-thread
+    draws; out-of-range chain ids and steps are rejected like the device's."""
+    from ip_mcmc_amd import IpmcError, _hostlib
+
+    a = _hostlib.pcn_draws(5, 0, 4096, 0, 8, 40, np.float64, np.ones(40), None, n_threads=8)
+    b = _hostlib.pcn_draws(5, 0, 4096, 0, 8, 40, np.float64, np.ones(40), None, n_threads=1)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    with pytest.raises(IpmcError, match="2\\^32"):
+        _hostlib.pcn_draws(5, 2**32 - 1, 2, 0, 1, 3, np.float64, np.ones(3), None)
+    with pytest.raises(IpmcError, match="2\\^63"):
+        _hostlib.pcn_draws(5, 0, 1, 2**63 - 1, 2, 3, np.float64, np.ones(3), None)
+    with pytest.raises(IpmcError, match="both NULL"):
+        _hostlib.pcn_draws(5, 0, 1, 0, 1, 3, np.float64, None, None)
+    u = _hostlib.extra_uniforms(5, 7, 11, 3)
+    assert u[0] == _hostlib.uniforms(5, 7, 1, 11)[0] and len(set(u)) == 3
 
 
 def _lin(golden):
@@ -353,3 +383,108 @@ def test_single_chain_float_loop_equals_array_loop(orc, odraws, golden, monkeypa
         else:
             assert np.array_equal(np.asarray(a), np.asarray(b))
     assert 0 < runs[0][2] < runs[0][1] < runs[0][3]
+
+
+# ------------------------------------------------ generic tier
+class _MyPCN(ProposerBase):
+    """proposer.py:59-82 restated as a caller's own class; `parts` splits the
+    draw into several multivariate_normal calls (a product prior that samples
+    its components one by one, distribution.py:57-59)."""
+
+    def __init__(self, beta, k, parts=(None,)):
+        self.beta, self.k, self.parts = beta, k, parts
+
+    def __call__(self, u, rng):
+        if self.parts == (None,):
+            w = rng.multivariate_normal(mean=np.zeros(self.k), cov=np.eye(self.k))
+        else:
+            w = np.concatenate([rng.multivariate_normal(mean=np.zeros(p), cov=np.eye(p)) for p in self.parts])
+        return np.sqrt(1 - self.beta**2) * u + self.beta * w
+
+
+def test_generic_tier_product_prior_draws_continue_the_stream(odraws, golden):
+    """Two multivariate_normal calls in one step get ξ[0:2] and ξ[2:4] (a
+    cursor), so a product prior equals the one-draw proposer: the lin_*
+    fixture again, and no two draws of a step are the same numbers."""
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    s = MCMCSampler(_MyPCN(beta, 4, parts=(2, 2)), CountedAccepter(pCNAccepter(pot)), PhiloxRNG(seed))
+    out = s.run(np.zeros((4, 4)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    assert s.last_path == "host-generic"
+    np.testing.assert_array_equal(out, golden["lin_samples"])
+
+
+def test_generic_tier_rng_cursor_and_unsupported_methods():
+    from ip_mcmc_amd import _hostlib
+
+    rng = hostloop.StepRNG(5)
+    xi = _hostlib.normals(5, 7, 1, 11, 3)[0]
+    rng.set(xi, _hostlib.uniforms(5, 7, 1, 11)[0], gid=7, step=11)
+    a = rng.standard_normal(2)
+    b = rng.normal(1.0, 2.0)  # the third component
+    c = rng.standard_normal(3)  # components 3..5 from the host library
+    full = _hostlib.normals(5, 7, 1, 11, 6)[0]
+    np.testing.assert_array_equal(a, full[:2])
+    assert b == 1.0 + 2.0 * full[2]
+    np.testing.assert_array_equal(c, full[3:6])
+    u0, u1, u2 = rng.random(), rng.random(), rng.uniform(2.0, 4.0)
+    ex = _hostlib.extra_uniforms(5, 7, 11, 3)
+    assert (u0, u1, u2) == (ex[0], ex[1], 2.0 + 2.0 * ex[2]) and u0 != u1
+    with pytest.raises(AttributeError, match="supports multivariate_normal"):
+        rng.gamma(2.0)
+
+
+def test_generic_tier_counts_decisions_without_a_counted_accepter(odraws, golden):
+    G, gamma, beta, seed, n_samples, burn_in, interval = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    s = MCMCSampler(_MyPCN(beta, 4), pCNAccepter(pot), PhiloxRNG(seed))
+    s.run(np.zeros((4, 4)), n_samples=n_samples, burn_in=burn_in, sample_interval=interval)
+    assert np.array_equal(s.state.accepts, golden["lin_counts"][:, 1])
+    assert s.state.accept_kind == "generic"
+
+
+class _MyVarPCN(ProposerBase):
+    """A stateful caller proposer (VarSteppCNProposer's pattern, proposer.py:
+    105-115: i incremented before use)."""
+
+    def __init__(self, k):
+        self.k, self.i = k, 0
+
+    def __call__(self, u, rng):
+        self.i += 1
+        beta = 0.5 / (1 + 0.1 * self.i)
+        w = rng.multivariate_normal(mean=np.zeros(self.k), cov=np.eye(self.k))
+        return np.sqrt(1 - beta**2) * u + beta * w
+
+
+def test_generic_tier_stateful_proposer_advances_once_per_step(odraws, golden):
+    """Several chains at once give each chain the schedule one chain would
+    see: the multi-chain run equals the chains run one at a time."""
+    G, gamma, _, seed, _, _, _ = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    many = MCMCSampler(_MyVarPCN(4), pCNAccepter(pot), PhiloxRNG(seed))
+    out = many.run(np.zeros((3, 4)), n_samples=5, burn_in=4, sample_interval=3)
+    assert many.proposer.i == 1 + 5 * 3
+    for c in range(3):
+        one = MCMCSampler(_MyVarPCN(4), pCNAccepter(pot), PhiloxRNG(seed), chain_offset=c)
+        np.testing.assert_array_equal(one.run(np.zeros(4), n_samples=5, burn_in=4, sample_interval=3), out[c])
+
+
+def test_generic_checkpoint_resumes_on_the_structured_tier_with_a_fresh_phi(odraws, golden):
+    """A generic run caches no Φ (NaN); resuming its state on a structured
+    sampler recomputes Φ(u) and continues exactly like a structured run from
+    the same states and Philox position."""
+    G, gamma, beta, seed, *_ = _lin(golden)
+    pot = EvolutionPotential(G, golden["lin_y"], GaussianDistribution(0, gamma**2))
+    prior = GaussianDistribution(np.zeros(4), np.eye(4))
+    g = MCMCSampler(_MyPCN(beta, 4), pCNAccepter(pot), PhiloxRNG(seed))
+    g.run(np.zeros((4, 4)), n_samples=3, burn_in=1, sample_interval=4)
+    st = g.checkpoint()
+    assert np.all(np.isnan(st.phi))
+    s = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(0))
+    a = s.run(st, n_samples=5, burn_in=0, sample_interval=2)
+    assert np.all(np.isfinite(s.state.phi))
+    ref = MCMCSampler(ConstSteppCNProposer(beta, prior), pCNAccepter(pot), PhiloxRNG(seed))
+    ref.rng.step = st.step
+    b = ref.run(st.u.copy(), n_samples=5, burn_in=0, sample_interval=2)
+    np.testing.assert_array_equal(a, b)

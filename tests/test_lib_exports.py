@@ -56,3 +56,20 @@ def test_struct_offsets_match_c_compiler(orc):
     want = [ctypes.sizeof(_abi.IpmcModel)] + [getattr(_abi.IpmcModel, f).offset for f, _ in _abi.IpmcModel._fields_]
     want += [ctypes.sizeof(_abi.IpmcSweep)] + [getattr(_abi.IpmcSweep, f).offset for f, _ in _abi.IpmcSweep._fields_]
     assert list(out[:n]) == want
+
+
+def test_libipmc_host_exports_every_declared_symbol():
+    """libipmc_host.so (include/ipmc_host.h) loads without a GPU or the HIP
+    runtime and exports exactly what its header declares."""
+    import subprocess
+
+    from ip_mcmc_amd import _hostlib
+
+    h = _hostlib.lib()
+    names = _declared("ipmc_host.h")
+    assert set(names) == set(_hostlib.SIGNATURES)
+    for name in names:
+        assert hasattr(h, name), name
+    assert h.ipmc_host_abi_version() == _hostlib.ABI_VERSION
+    deps = subprocess.run(["ldd", _hostlib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "amdhip64" not in deps and "libhsa" not in deps, deps
