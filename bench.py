@@ -1,31 +1,39 @@
 """Headline benchmark: pCN steps/s on Lorenz-96 d=40, 2000 RK4 steps, 65 536 chains.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--workload cfg3|cfg4|cfg5]
   (N > 1: started once, it launches torch.distributed.run with N ranks itself;
    under an external torch.distributed.run WORLD_SIZE must equal N)
 
-A "step" is one pCN step of every chain of the batch: propose, run the forward
-map (2000 RK4 steps of Lorenz-96, d=40), evaluate Φ, accept or reject -- the
-fused libipmc kernel.  The metric's 65 536 chains are split over the N GPUs
-(strong scaling, the default; global chain ids rank*65536/N + i); the weak
-number (65 536 chains per GPU) is carried in "extra" for N > 1.  When a GPU
-holds fewer chains than fill it, one launch runs several pCN steps
-(--steps-per-launch, auto), so the speculative sweep can fill the lanes;
-results are bit-identical to one step per launch.  Inputs are resident in HBM
-before the timed region.  value = all chains of all ranks x K / max-rank wall
-time.  Arithmetic: float64 with the FMA forward map (the reference computes in
-float64); "extra" carries float32, the REFERENCE-arith (no FMA, the
-reference's operation order) throughput, and MCMCSampler.run end to end
-(host u_0 in, samples back on the host).
+A "step" is one pCN step of every chain of the ensemble: propose, run the
+forward map (cfg3: 2000 RK4 steps of Lorenz-96, d=40), evaluate Φ, accept or
+reject.  value is SURVEY §8(d)'s timed region: the drop-in
+``MCMCSampler.run`` end to end, through the sharded entry point
+``shard.run_sharded`` -- host u_0 in (H2D), Φ(u_0), exactly K pCN steps of
+every chain in the fused libipmc kernels, the posterior-mean sums and the
+chain state back to the host (D2H), and the final gather over the ranks
+(RCCL at N > 1) -- bracketed by barrier + synchronize, max over ranks.
+value = all chains of all ranks x K / that time.  The metric's 65 536 chains
+are split over the N GPUs (strong scaling, the default; global chain ids, so
+every chain is the one-GPU run's bit for bit); the weak number (65 536 chains
+per GPU) is carried in "extra" for N > 1.
+
+extra.kernel_*: the same sweep kernel on device-resident state (raw
+ipmc_pcn_sweep launches, one pCN step per launch for a full GPU, HIP events
+on the launch stream) -- the number the roofline is computed on.
 
 roofline: VALU-bound (no MFMA, no HBM traffic inside the RK loop). achieved =
-algorithmic FLOP per launch / average kernel time from HIP events on the
-launch stream; algorithmic FLOP per pCN step per chain = 30·d·n = 2.4 MFLOP
-(SURVEY §8(d) counting rule).
+algorithmic FLOP per launch / average kernel time of the kernel leg's timed
+launches; algorithmic FLOP per pCN step per chain = 30·d·n (SURVEY §8(d)
+counting rule).
 cpu_baseline: the C oracle (same arithmetic, bit-exact), a bounded sample of
 the same workload on this host's cores, rank 0 at N=1 only; the reference
 itself, timed in the build container by tools/reference_cpu_baseline.py, is
 attached as cpu_baseline.reference_recorded.
+
+--workload cfg4 / cfg5 times BASELINE's configs 4 (viscous Burgers N=256,
+1 000 FD steps, 16 384 chains over the node) and 5 (Lorenz-96 d=256, 10 000
+RK4 steps, 2^20 chains over the node, fp32 beside fp64) the same way; the
+default cfg3 line carries short end-to-end runs of both in extra.configs.
 """
 import argparse
 import ctypes as C
@@ -43,39 +51,80 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from ip_mcmc_amd import Lorenz96Operator, _abi  # noqa: E402
+from ip_mcmc_amd import BurgersOperator, Lorenz96Operator, _abi  # noqa: E402
 from ip_mcmc_amd._lib import call  # noqa: E402
 
-D, N_RK, DT, BETA, GAMMA = 40, 2000, 0.005, 0.2, 0.1
 ITEM = {"f64": 8, "f32": 4}
-# 30 algorithmic FLOP per component and RK4 step in 20 VALU ops (10 of them
-# FMA): at most 30 / (2 x 20) of the all-FMA peak
-MIX_CEILING = 30 / 40
-CHAINS_PER_GPU = 65536
-FLOP_PER_STEP = 30 * D * N_RK  # 2.4e6
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}  # MI355X vector (spec), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+CHAINS_PER_GPU = 65536  # cfg3's metric ensemble (the weak-scaling share)
+METRIC = "pCN steps/sec (whole node), Lorenz-96 d=40 T=2000, 65 536 chains"
 
 
-def problem():
-    """Config 3: forcing-field inverse problem."""
-    op = Lorenz96Operator(D, forcing_mean=8.0, dt=DT, n_steps=N_RK)  # x0: 1000-step spin-up from 8 + 0.01 e0
-    k = np.arange(D)
-    u_true = 0.5 * np.sin(2 * np.pi * k / D)  # F_true = 8 + 0.5 sin(2πk/40)
-    g_true = op(u_true)
-    y = g_true + GAMMA * np.random.default_rng(3).normal(size=D)
-    return op, y
+class Problem:
+    """One BASELINE workload: forward map, data, noise, prior and pCN step."""
+
+    def __init__(self, key, name, op, y, gamma, prior_sqrt, beta, chains, flop, mix_ceiling, steps, warmup, data):
+        self.key, self.name, self.op, self.y = key, name, op, np.asarray(y, dtype=np.float64)
+        self.gamma = np.broadcast_to(np.asarray(gamma, dtype=np.float64), self.y.shape).copy()
+        self.sq = np.asarray(prior_sqrt, dtype=np.float64)
+        self.beta, self.chains, self.flop = beta, chains, flop
+        self.mix_ceiling, self.steps, self.warmup, self.data = mix_ceiling, steps, warmup, data
+        self.k = op.k
+
+    def reference_arith(self):
+        """The same problem with the forward map in REFERENCE arith (no FMA, the
+        reference's operation order; Lorenz-96 only)."""
+        import copy
+
+        p = copy.copy(self)
+        o = self.op
+        p.op = Lorenz96Operator(o.K, forcing_mean=o.theta0, x0=o.x0, dt=o.dt, n_steps=o.n_steps, arith="reference")
+        return p
 
 
+def make_problem(key):
+    """cfg3 (the headline), cfg4, cfg5 of BASELINE.json / SURVEY §8(d)."""
+    if key == "cfg3":
+        d, n = 40, 2000
+        op = Lorenz96Operator(d, forcing_mean=8.0, dt=0.005, n_steps=n)  # x0: 1000-step spin-up from 8 + 0.01 e0
+        k = np.arange(d)
+        y = op(0.5 * np.sin(2 * np.pi * k / d)) + 0.1 * np.random.default_rng(3).normal(size=d)
+        # 30 algorithmic FLOP per component and RK4 step in 20 VALU ops (10 of
+        # them FMA): at most 30 / (2 x 20) of the all-FMA peak (DESIGN.md §5)
+        return Problem(key, "lorenz96_d40_rk4_2000_pcn", op, y, 0.1, np.ones(d), 0.2, 65536, 30 * d * n, 30 / 40,
+                       200, 10, "synthetic (forcing-field inverse problem, F = 8 + u, y = G(0.5 sin(2 pi k/40)) + "
+                       "N(0, 0.1^2), seed 3; prior N(0, I); u_0 = 0)")
+    if key == "cfg4":
+        # burgers_beta.py:25-87 at N=256 (SURVEY §8(d) cfg 4), viscous (nu = 1e-3), fixed dt 1e-3 x 1 000
+        op = BurgersOperator(N=256, dt_mode="fixed", dt=1e-3, n_steps=1000, nu=1e-3)
+        y = op(np.array([0.025, -0.025, -0.02])) + 0.05 * np.random.default_rng(3).normal(size=5)
+        return Problem(key, "burgers_n256_fd1000_viscous_pcn", op, y, 0.05, np.full(3, 0.25), 0.15, 16384,
+                       30 * 256 * 1000, None, 100, 5, "synthetic (Riemann-IC inverse problem, theta = [1.5, 0.25, "
+                       "-0.5] + u, y = G([0.025, -0.025, -0.02]) + N(0, 0.05^2), seed 3; prior N(0, 0.25^2 I))")
+    if key == "cfg5":
+        d, n = 256, 10000
+        op = Lorenz96Operator(d, forcing_mean=8.0, dt=0.005, n_steps=n)
+        k = np.arange(d)
+        y = op(0.5 * np.sin(2 * np.pi * k / d)) + 0.1 * np.random.default_rng(3).normal(size=d)
+        return Problem(key, "lorenz96_d256_rk4_10000_pcn", op, y, 0.1, np.ones(d), 0.2, 1 << 20, 30 * d * n, 30 / 40,
+                       4, 1, "synthetic (forcing-field inverse problem, d=256, y = G(0.5 sin(2 pi k/256)) + "
+                       "N(0, 0.1^2), seed 3; prior N(0, I); u_0 = 0)")
+    raise SystemExit(f"unknown workload {key}")
+
+
+# ------------------------------------------------------------ kernel leg
 class Workload:
-    def __init__(self, op, y, n_chains, chain_offset, dtype, dev, lanes=0, d=D, chains_per_lane=0, per_launch=1,
+    """Device-resident chains swept by raw ipmc_pcn_sweep launches (the kernel leg)."""
+
+    def __init__(self, prob, n_chains, chain_offset, dtype, dev, lanes=0, chains_per_lane=0, per_launch=1,
                  spec_width=0):
         self.dev, self.dtype = dev, dtype
         self.n_chains, self.per_launch = n_chains, per_launch
-        self.model, self._keep = op.model(dtype, dev)
+        self.model, self._keep = prob.op.model(dtype, dev)
         t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dtype).to(dev).contiguous()
-        self.y, self.ginv, self.sq = t(y), t(np.full(d, 1 / GAMMA)), t(np.ones(d))
-        self.u = torch.zeros((n_chains, d), dtype=dtype, device=dev)
+        self.y, self.ginv, self.sq = t(prob.y), t(1.0 / prob.gamma), t(prob.sq)
+        self.u = torch.zeros((n_chains, prob.k), dtype=dtype, device=dev)
         self.phi = torch.empty(n_chains, dtype=dtype, device=dev)
         self.acc = torch.zeros(n_chains, dtype=torch.int64, device=dev)
         self.stream = torch.cuda.current_stream(dev).cuda_stream
@@ -87,7 +136,7 @@ class Workload:
         s.n_chains, s.chain_offset = n_chains, chain_offset
         s.u, s.phi, s.accepts = self.u.data_ptr(), self.phi.data_ptr(), self.acc.data_ptr()
         s.y, s.gamma_inv, s.prior_sqrt = self.y.data_ptr(), self.ginv.data_ptr(), self.sq.data_ptr()
-        s.beta, s.contraction = BETA, float(np.sqrt(1 - BETA**2))
+        s.beta, s.contraction = prob.beta, float(np.sqrt(1 - prob.beta**2))
         s.seed, s.step0, s.n_steps = 2, 0, per_launch
         self.s = s
         # the plan the sweep runs (ipmc_plan_sweep: same code path as the launch)
@@ -132,7 +181,7 @@ def sweep_plan(model, sweep):
     return p.lanes_per_chain, p.chains_per_lane, p.spec_width
 
 
-def pmc_record(dtype, chains, lanes):
+def pmc_record(dtype, chains, lanes, d=40, n_rk=2000):
     """The committed rocprofv3 PMC passes of this sweep kernel (same dtype,
     chains, shape and lanes-per-chain layout): profiles/r*/pmc_l96_<dtype>.json,
     newest round first -- HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE,
@@ -143,8 +192,8 @@ def pmc_record(dtype, chains, lanes):
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"pmc_l96_{dtype}.json")), reverse=True):
         rec = json.load(open(path))
         names = " ".join(rec.get("kernel", []))
-        if (rec.get("chains") == chains and rec.get("d") == D and rec.get("rk4_steps") == N_RK
-                and f"{D}, {lanes}, true" in names):
+        if (rec.get("chains") == chains and rec.get("d") == d and rec.get("rk4_steps") == n_rk
+                and f"{d}, {lanes}, true" in names):
             return rec, os.path.relpath(path, REPO)
     return None, None
 
@@ -195,24 +244,121 @@ def timed(w, steps, warmup, world, settle_s=0.0):
     return max_over_ranks(el, world, w.dev), kern_ms
 
 
-def cpu_baseline(op, y, dtype_np, budget_s=15.0):
+# --------------------------------------------------------- end-to-end leg
+def sampler_factory(prob, dtype_np, dev, seed=2):
+    """make(chain_offset) -> the drop-in sampler of `prob` (the reference's
+    composition: ConstSteppCNProposer + pCNAccepter(EvolutionPotential))."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, MCMCSampler, PhiloxRNG,
+                             pCNAccepter)
+
+    prior = GaussianDistribution(np.zeros(prob.k), np.diag(prob.sq**2))
+    noise = GaussianDistribution(np.zeros(prob.y.shape[0]), np.diag(prob.gamma**2))
+
+    def make(chain_offset=0):
+        pot = EvolutionPotential(prob.op, prob.y, noise)
+        return MCMCSampler(ConstSteppCNProposer(prob.beta, prior), pCNAccepter(pot), PhiloxRNG(seed),
+                           dtype=dtype_np, device=dev, chain_offset=chain_offset)
+
+    return make
+
+
+def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="all", seed=2):
+    """SURVEY §8(d)'s timed region: shard.run_sharded(u_0 on the host, exactly
+    `steps` pCN steps, keep='moments') bracketed by barrier + synchronize,
+    after an untimed run of `warmup` steps of the same shape.  Returns the
+    record and the gathered result."""
+    from ip_mcmc_amd.shard import run_sharded
+
+    make = sampler_factory(prob, dtype_np, dev, seed)
+    u0 = np.full((total_chains, prob.k), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch)
+    if warmup > 0:
+        run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=warmup, keep="moments", gather=gather)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    res = run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=steps, keep="moments", gather=gather)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    smp = res["sampler"]
+    assert smp.last_path == "device" and smp.state.steps_this_run == steps
+    tm = smp.last_run_timing
+    rec = {"pcn_steps_per_s": total_chains * steps / el, "wall_s": el, "ms_per_step": el / steps * 1e3,
+           "steps": steps, "total_chains": total_chains, "chains_per_gpu": total_chains // world,
+           "accept_rate": float(res["accepts"].sum()) / (total_chains * steps),
+           "run_seconds_rank0": res["run_seconds"], "gather_ms": res["gather_seconds"] * 1e3,
+           "setup_ms": tm["setup_s"] * 1e3, "sweeps_gpu_ms": tm["sweeps_gpu_ms"], "tail_ms": tm["tail_ms"]}
+    return rec, res
+
+
+def e2e_samples(prob, n_chains, chain_offset, dtype_np, dev, world, n_samples=20):
+    """MCMCSampler.run with samples: host u_0 (n_chains x k) in, n_samples
+    samples 1 step apart back on the host (page-locked, copied in blocks while
+    later blocks sweep)."""
+    make = sampler_factory(prob, dtype_np, dev)
+    s = make(chain_offset)
+    u0 = np.full((n_chains, prob.k), 0.0)
+    # warm run of the same size: device allocations, and the page-locked result
+    # block that torch's host allocator recycles once the caller drops it
+    s.run(u0, n_samples=n_samples, burn_in=1, sample_interval=1)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    t0 = time.perf_counter()
+    out = s.run(u0, n_samples=n_samples, burn_in=1, sample_interval=1)
+    el = time.perf_counter() - t0
+    assert out.shape == (n_chains, n_samples, prob.k)
+    barrier(world)
+    el_max = max_over_ranks(el, world, dev)
+    tm = s.last_run_timing
+    return {"pcn_steps_per_s": world * n_chains * n_samples / el_max, "wall_s": el_max, "samples": n_samples,
+            "sample_bytes_per_rank": int(out.nbytes), "setup_ms": tm["setup_s"] * 1e3,
+            "sweeps_gpu_ms": tm["sweeps_gpu_ms"], "tail_ms_after_sweeps": tm["tail_ms"],
+            "copy_overlapped": tm["copy_overlapped"],
+            "note": "MCMCSampler.run(u0 host (chains x k), n_samples, burn_in=1, sample_interval=1): H2D of u0, "
+                    "Phi(u0), the sweeps, D2H of the (chains, n_samples, k) f64 samples; tail = wall after set-up "
+                    "not covered by the GPU sweeps (launch gaps + the last copy block + epilogue)"}
+
+
+def config_line(key, dev, world, steps=None, warmup=None, chains=None):
+    """A short end-to-end run of config 4 or 5 as BASELINE states it (the
+    ensemble over the node): f64, and for config 5 f32 beside it with the
+    posterior-mean difference of the two short runs in between-chain standard
+    errors (a smoke of the fp32-vs-fp64 comparison; the stated tolerance is
+    the stationary test, tests/test_gpu_tolerance.py)."""
+    prob = make_problem(key)
+    total = chains or prob.chains
+    st, wu = steps or prob.steps, prob.warmup if warmup is None else warmup
+    gather = "mean" if key == "cfg5" else "all"
+    rec64, r64 = timed_run(prob, np.float64, dev, total, st, wu, world, gather=gather)
+    out = {"workload": prob.name, "f64": rec64, "flop_per_chain_step": prob.flop,
+           "tflops_f64": total * prob.flop * st / rec64["wall_s"] / 1e12}
+    if key == "cfg5":
+        rec32, r32 = timed_run(prob, np.float32, dev, total, st, wu, world, gather=gather, seed=3)
+        out["f32"] = rec32
+        out["tflops_f32"] = total * prob.flop * st / rec32["wall_s"] / 1e12
+        out["f32_over_f64"] = rec32["pcn_steps_per_s"] / rec64["pcn_steps_per_s"]
+        out["posterior_mean_max_abs_diff_f32_f64"] = float(np.max(np.abs(r32["mean"] - r64["mean"])))
+    return out
+
+
+def cpu_baseline(prob, dtype_np, budget_s=15.0):
     """The C oracle on this host's cores: a bounded sample of the same
     workload (chains x 1 pCN step), scaled to pCN steps/s."""
-    sys.path.insert(0, REPO)
     from oracle import oracle as O
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
-
-    ginv = np.full(D, 1 / GAMMA)
-    phi0 = O.potential(op, np.zeros((1, D), dtype=dtype_np), y, ginv, dtype_np)[0]
+    ginv = 1.0 / prob.gamma
+    phi0 = O.potential(prob.op, np.zeros((1, prob.k), dtype=dtype_np), prob.y, ginv, dtype_np)[0]
 
     def run(nc):
-        U = np.zeros((nc, D), dtype=dtype_np)  # every chain starts at u = 0, as on the GPU
+        U = np.zeros((nc, prob.k), dtype=dtype_np)  # every chain starts at u = 0, as on the GPU
         phi = np.full(nc, phi0, dtype=dtype_np)
         acc = np.zeros(nc, dtype=np.int64)
         t0 = time.perf_counter()
-        O.pcn_sweep(op, U, phi, y, ginv, np.ones(D), BETA, 2, 0, 1, accepts=acc, n_threads=threads)
+        O.pcn_sweep(prob.op, U, phi, prob.y, ginv, prob.sq, prob.beta, 2, 0, 1, accepts=acc, n_threads=threads)
         return time.perf_counter() - t0
 
     t1 = run(threads)  # one chain-step per thread, calibration
@@ -221,8 +367,8 @@ def cpu_baseline(op, y, dtype_np, budget_s=15.0):
     n = (n // threads) * threads
     el = run(n)
     return {"value": n / el, "unit": "pCN steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} chains x 1 pCN step of the headline workload (d=40, 2000 RK4 steps, "
-                      f"{'f64' if dtype_np == np.float64 else 'f32'}), C oracle, {threads} threads, {el:.1f} s"}
+            "sample": f"{n} chains x 1 pCN step of the {prob.name} workload "
+                      f"({'f64' if dtype_np == np.float64 else 'f32'}), C oracle, {threads} threads, {el:.1f} s"}
 
 
 def _free_port():
@@ -245,62 +391,34 @@ def launch_ranks(n):
 
 
 def auto_per_launch(chains_per_rank):
-    """pCN steps per launch: 1 when the rank's chains fill a wave per SIMD on
-    their own (>= 16 384 chains, one launch per step), else 512, so that the
-    sweep speculates over the steps of a launch (ipmc_plan_sweep).  A launch
-    lasts as long as its slowest chain, so short speculative launches lose to
-    the chains that accept early: 8 192 chains run sequentially on 8
-    interleaved lanes below 256 steps per launch and speculate on 4 lanes x 2
-    slots from there (ipmc_plan_sweep): 14.4 / 16.6 / 17.8 M steps/s on this
-    problem at 20 / 200 / 1 024 timed steps, where round 3's first rule (2
-    lanes x 8 slots) ran 5.9 / 15.6 / 18.9 M (profiles/r3/bench_8192_*.jsonl)."""
+    """pCN steps per launch of the kernel leg: 1 when the rank's chains fill a
+    wave per SIMD on their own (>= 16 384 chains, one launch per step), else
+    512, so that the sweep speculates over the steps of a launch
+    (ipmc_plan_sweep).  A launch lasts as long as its slowest chain, so short
+    speculative launches lose to the chains that accept early: 8 192 chains
+    run sequentially on 8 interleaved lanes below 256 steps per launch and
+    speculate on 4 lanes x 2 slots from there (ipmc_plan_sweep): 14.4 / 16.6 /
+    17.8 M steps/s on this problem at 20 / 200 / 1 024 timed steps, where round
+    3's first rule (2 lanes x 8 slots) ran 5.9 / 15.6 / 18.9 M
+    (profiles/r3/bench_8192_*.jsonl)."""
     return 1 if chains_per_rank >= 16384 else 512
-
-
-def e2e_run(op, y, n_chains, chain_offset, dtype_np, dev, world, n_samples=20):
-    """MCMCSampler.run end to end (SURVEY §8(d)'s timed region): host u_0
-    (n_chains x 40) in, n_samples samples 1 step apart back on the host
-    (page-locked, copied in blocks while later blocks sweep)."""
-    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, MCMCSampler,
-                             PhiloxRNG, pCNAccepter)
-
-    prior = GaussianDistribution(np.zeros(D), np.eye(D))
-    pot = EvolutionPotential(op, y, GaussianDistribution(np.zeros(D), GAMMA**2 * np.eye(D)))
-    u0 = np.full((n_chains, D), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch, inside run())
-    s = MCMCSampler(ConstSteppCNProposer(BETA, prior), pCNAccepter(pot), PhiloxRNG(2), dtype=dtype_np, device=dev,
-                    chain_offset=chain_offset)
-    # warm run of the same size: device allocations, and the page-locked result
-    # block that torch's host allocator recycles once the caller drops it
-    s.run(u0, n_samples=n_samples, burn_in=1, sample_interval=1)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    t0 = time.perf_counter()
-    out = s.run(u0, n_samples=n_samples, burn_in=1, sample_interval=1)
-    el = time.perf_counter() - t0
-    assert out.shape == (n_chains, n_samples, D)
-    barrier(world)
-    el_max = max_over_ranks(el, world, dev)
-    tm = s.last_run_timing
-    return {"pcn_steps_per_s": world * n_chains * n_samples / el_max, "wall_s": el_max, "samples": n_samples,
-            "sample_bytes_per_rank": int(out.nbytes), "setup_ms": tm["setup_s"] * 1e3,
-            "sweeps_gpu_ms": tm["sweeps_gpu_ms"], "tail_ms_after_sweeps": tm["tail_ms"],
-            "copy_overlapped": tm["copy_overlapped"],
-            "note": "MCMCSampler.run(u0 host (chains x 40), n_samples, burn_in=1, sample_interval=1): H2D of u0, "
-                    "Phi(u0), the sweeps, D2H of the (chains, n_samples, 40) f64 samples; tail = wall after set-up "
-                    "not covered by the GPU sweeps (launch gaps + the last copy block + epilogue)"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--chains", type=int, default=CHAINS_PER_GPU,
-                    help="total chains (strong, the default) or chains per GPU (weak)")
+    ap.add_argument("--steps", type=int, default=None, help="timed pCN steps (default: the workload's, cfg3 200)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed pCN steps first (default: cfg3 10)")
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg4", "cfg5"],
+                    help="cfg3: the headline (Lorenz-96 d=40, 65 536 chains); cfg4: viscous Burgers N=256, 16 384 "
+                         "chains; cfg5: Lorenz-96 d=256, 10 000 RK4 steps, 2^20 chains (f32 beside f64)")
+    ap.add_argument("--chains", type=int, default=None,
+                    help="total chains (strong, the default) or chains per GPU (weak); default: the workload's")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="strong: --chains split over the GPUs (the metric's 65 536; default); "
                          "weak: --chains per GPU")
-    ap.add_argument("--steps-per-launch", type=int, default=0, help="pCN steps per kernel launch (0 = auto)")
+    ap.add_argument("--steps-per-launch", type=int, default=0,
+                    help="pCN steps per kernel launch of the kernel leg (0 = auto)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--lanes", type=int, default=0)
     ap.add_argument("--spec-width", type=int, default=0, help="speculative slots per chain (0 = auto, 1 = off)")
@@ -308,6 +426,7 @@ def main():
                     help="seconds of untimed G evaluations before the warm-up steps (clock ramp; 0 = off)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the short cfg4 / cfg5 runs in extra.configs")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the product path) or gloo (rehearsal of the N-rank logic)")
     ap.add_argument("--share-device", action="store_true",
@@ -334,123 +453,138 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    log(f"rank {rank}/{world} on {dev}: building the problem")
-    op, y = problem()
-    total_chains = args.chains * (world if args.scaling == "weak" else 1)
+    log(f"rank {rank}/{world} on {dev}: building the {args.workload} problem")
+    prob = make_problem(args.workload)
+    steps = args.steps if args.steps is not None else prob.steps
+    warmup = args.warmup if args.warmup is not None else prob.warmup
+    chains = args.chains or prob.chains
+    total_chains = chains * (world if args.scaling == "weak" else 1)
     if total_chains % world:
         raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
     per_rank = total_chains // world
-    # (a launch never exceeds the timed steps: the plan reported is the one timed)
-    per_launch = min(args.steps_per_launch or auto_per_launch(per_rank), max(1, args.steps))
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
-    w = Workload(op, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch,
+    ndt = np.float64 if args.dtype == "f64" else np.float32
+
+    # 1. kernel leg: device-resident sweeps, HIP events (the roofline's kernel time)
+    # (a launch never exceeds the timed steps: the plan reported is the one timed)
+    per_launch = min(args.steps_per_launch or auto_per_launch(per_rank), max(1, steps))
+    w = Workload(prob, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch,
                  spec_width=args.spec_width)
-    log(f"timing {args.steps} pCN steps ({args.dtype}, {per_rank} chains/GPU, {per_launch} steps/launch, "
+    log(f"kernel leg: {steps} pCN steps ({args.dtype}, {per_rank} chains/GPU, {per_launch} steps/launch, "
         f"lanes={w.lanes}, spec_width={w.spec_width})")
-    el, kern_ms = timed(w, args.steps, args.warmup, world, args.settle)
-    log(f"{args.dtype}: {el:.3f} s, kernel {kern_ms:.3f} ms/launch")
-    value = total_chains * args.steps / el
+    el_k, kern_ms = timed(w, steps, warmup, world, args.settle)
+    kernel_rate = total_chains * steps / el_k
+    log(f"kernel leg: {el_k:.3f} s, kernel {kern_ms:.3f} ms/launch, {kernel_rate / 1e6:.2f} M steps/s")
+    lanes_k, cpl_k, spec_k = w.lanes, w.chains_per_lane, w.spec_width
+    del w
 
-    # final gather of the per-chain results (the path's one exchange): accept
-    # rate and posterior-mean state over all chains of all ranks
-    from ip_mcmc_amd.shard import gather_chains
-
-    # (after the timed region: per-chain state u, Φ and accept counts of every
-    # rank to every rank; all_gather_into_tensor = RCCL over xGMI at N > 1)
-    torch.cuda.synchronize(w.dev)
-    barrier(world)
-    tg = time.perf_counter()
-    host = (lambda t: t.cpu()) if args.dist_backend == "gloo" else (lambda t: t)
-    u_all = gather_chains(host(w.u), total_chains)
-    phi_all = gather_chains(host(w.phi.view(-1, 1)), total_chains)
-    acc_all = gather_chains(host(w.acc.view(-1, 1)), total_chains)
-    torch.cuda.synchronize(w.dev)
-    gather_ms = (time.perf_counter() - tg) * 1e3
-    gather = {"ms": gather_ms, "bytes_per_rank": int(w.u.numel() * w.u.element_size() + w.phi.numel() *
-                                                     w.phi.element_size() + w.acc.numel() * 8),
+    # 2. value: MCMCSampler.run end to end through shard.run_sharded
+    gather_mode = "mean" if total_chains * prob.k > (1 << 26) else "all"
+    log(f"end-to-end leg: run_sharded({total_chains} chains, {steps} steps, keep='moments', gather={gather_mode})")
+    e2e, res = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode)
+    value = e2e["pcn_steps_per_s"]
+    log(f"end-to-end: {e2e['wall_s']:.3f} s, {value / 1e6:.2f} M steps/s")
+    gather = {"ms": e2e["gather_ms"], "mode": gather_mode,
+              "bytes_per_rank": int(per_rank * (3 * prob.k + 2) * 8 if gather_mode == "all" else per_rank * 16),
               "collective": (f"all_gather_into_tensor ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
+                             + (" + rank-sequential ordered sum (send/recv)" if gather_mode == "mean" else "")
                              if world > 1 else "none (one rank)"),
-              "rows": int(u_all.shape[0])}
-    assert bool(torch.isfinite(phi_all).all())
-    del u_all, phi_all
-    accept_rate = float(acc_all.double().sum().item()) / (total_chains * (args.steps + args.warmup))
+              "rows": int(res["phi"].shape[0]), "inside_timed_region": True}
+    assert np.isfinite(res["phi"]).all() and np.isfinite(res["mean"]).all()
+    accept_rate = e2e["accept_rate"]
+    del res
 
-    extra = {}
-    if not args.no_extra:
+    extra = {"kernel_pcn_steps_per_s": kernel_rate, "kernel_ms": kern_ms,
+             "kernel_note": "device-resident state, raw ipmc_pcn_sweep launches of steps_per_launch steps, HIP "
+                            "events on the launch stream (the roofline's kernel time); no H2D / D2H / gather",
+             "run_e2e_moments": e2e}
+    if not args.no_extra and args.workload == "cfg3":
         # one-step launches: 40 steps are plenty; speculative launches (small
         # shards) are timed over the headline's steps, as short ones are slow
-        xs = min(args.steps, 40) if per_launch == 1 else args.steps
+        xs = min(steps, 40) if per_launch == 1 else steps
         other = torch.float32 if tdt == torch.float64 else torch.float64
         key = "f32" if other == torch.float32 else "f64"
-        w2 = Workload(op, y, per_rank, rank * per_rank, other, dev, args.lanes, per_launch=per_launch)
+        w2 = Workload(prob, per_rank, rank * per_rank, other, dev, args.lanes, per_launch=per_launch)
         el2, k2 = timed(w2, xs, 2, world)
         log(f"{key}: kernel {k2:.3f} ms/launch")
-        extra[f"{key}_pcn_steps_per_s"] = total_chains * xs / el2
+        extra[f"{key}_kernel_pcn_steps_per_s"] = total_chains * xs / el2
         extra[f"{key}_kernel_ms"] = k2
-        extra[f"{key}_tflops"] = per_rank * per_launch * FLOP_PER_STEP / (k2 * 1e-3) / 1e12
+        extra[f"{key}_kernel_tflops"] = per_rank * per_launch * prob.flop / (k2 * 1e-3) / 1e12
         del w2
+        e2 = timed_run(prob, np.float32 if key == "f32" else np.float64, dev, total_chains, min(steps, 100), 2,
+                       world, gather=gather_mode)[0]
+        extra[f"{key}_run_pcn_steps_per_s"] = e2["pcn_steps_per_s"]
         # the reference's operation order (no FMA in the forward map): the
         # arithmetic whose accept streams are pinned to the reference fixtures
-        op_ref = Lorenz96Operator(D, forcing_mean=8.0, x0=op.x0, dt=DT, n_steps=N_RK, arith="reference")
-        w3 = Workload(op_ref, y, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch)
+        pref = prob.reference_arith()
+        w3 = Workload(pref, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch)
         xr = min(xs, 20) if per_launch == 1 else xs
         el3, k3 = timed(w3, xr, 2, world)
         log(f"reference arith ({args.dtype}): kernel {k3:.3f} ms/launch")
-        extra["reference_arith_pcn_steps_per_s"] = total_chains * xr / el3
+        extra["reference_arith_kernel_pcn_steps_per_s"] = total_chains * xr / el3
         extra["reference_arith_kernel_ms"] = k3
-        extra["reference_arith_tflops"] = per_rank * per_launch * FLOP_PER_STEP / (k3 * 1e-3) / 1e12
+        extra["reference_arith_kernel_tflops"] = per_rank * per_launch * prob.flop / (k3 * 1e-3) / 1e12
         del w3
         if world > 1:  # weak scaling beside the strong line: 65 536 chains per GPU
-            w4 = Workload(op, y, CHAINS_PER_GPU, rank * CHAINS_PER_GPU, tdt, dev, args.lanes, per_launch=1)
-            el4, k4 = timed(w4, xs, 2, world)
-            extra["weak_scaling"] = {"pcn_steps_per_s": world * CHAINS_PER_GPU * xs / el4,
-                                     "total_chains": world * CHAINS_PER_GPU, "ms_per_step": el4 / xs * 1e3,
-                                     "kernel_ms": k4, "steps": xs}
-            del w4
-        extra["run_e2e"] = e2e_run(op, y, per_rank, rank * per_rank, np.float64 if tdt == torch.float64
-                                   else np.float32, dev, world)
-        extra["run_e2e_pcn_steps_per_s"] = extra["run_e2e"]["pcn_steps_per_s"]
+            wk, _ = timed_run(prob, ndt, dev, world * CHAINS_PER_GPU, min(steps, 40), 2, world, gather=gather_mode)
+            extra["weak_scaling"] = {"pcn_steps_per_s": wk["pcn_steps_per_s"], "total_chains": world * CHAINS_PER_GPU,
+                                     "ms_per_step": wk["ms_per_step"], "steps": wk["steps"],
+                                     "timed": "run_sharded end to end, keep='moments'"}
+        extra["run_e2e_samples"] = e2e_samples(prob, per_rank, rank * per_rank, ndt, dev, world)
+    if not args.no_configs and args.workload == "cfg3":
+        cfgs = {}
+        for key in ("cfg4", "cfg5"):
+            log(f"extra.configs: {key} end to end")
+            cfgs[key] = config_line(key, dev, world)
+        extra["configs"] = cfgs
 
-    flop = per_rank * per_launch * FLOP_PER_STEP
+    flop = per_rank * per_launch * prob.flop
     achieved = flop / (kern_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    pmc, pmc_src = pmc_record(args.dtype, per_rank, w.lanes) if per_launch == 1 else (None, None)
+    is_l96_40 = args.workload == "cfg3"
+    pmc, pmc_src = pmc_record(args.dtype, per_rank, lanes_k) if (per_launch == 1 and is_l96_40) else (None, None)
     traffic = None if pmc is None else pmc["hbm_bytes_per_launch"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         log("CPU baseline (C oracle)")
-        cpu = cpu_baseline(op, y, np.float64 if tdt == torch.float64 else np.float32)
-        ref_rec = os.path.join(REPO, "profiles", "r1", "reference_cpu_cfg3.json")
-        if os.path.exists(ref_rec):  # the reference itself, timed in the build container (tools/)
-            cpu["reference_recorded"] = json.load(open(ref_rec))
+        cpu = cpu_baseline(prob, ndt)
+        import glob
+
+        recs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "reference_cpu_cfg3.json")), reverse=True)
+        if is_l96_40 and recs:  # the reference itself, timed in the build container (tools/), newest round
+            cpu["reference_recorded"] = json.load(open(recs[0]))
+            cpu["reference_recorded"]["source"] = os.path.relpath(recs[0], REPO)
 
     if rank == 0:
+        item = ITEM[args.dtype]
         line = {
-            "metric": "pCN steps/sec (whole node), Lorenz-96 d=40 T=2000, 65 536 chains",
+            "metric": METRIC if args.workload == "cfg3" else f"pCN steps/sec (whole node), {prob.name}, "
+                                                             f"{total_chains} chains",
             "value": value,
             "unit": "pCN steps/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": e2e["ms_per_step"],
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic (forcing-field inverse problem, y = G(u_true) + N(0, 0.1^2), seed 3)",
+            "data": prob.data,
             "config": {
-                "workload": "lorenz96_d40_rk4_2000_pcn",
+                "workload": prob.name,
+                "timed": "shard.run_sharded -> MCMCSampler.run(u_0 host (chains x k) f64, n_samples=1, burn_in=0, "
+                         "sample_interval=steps, keep='moments') end to end: H2D of u_0, Phi(u_0), the fused sweeps, "
+                         "D2H of the state and the posterior-mean sums, the gather over ranks; max over ranks",
                 "chains_per_gpu": per_rank,
                 "total_chains": total_chains,
-                "d": D,
-                "rk4_steps": N_RK,
-                "dt": DT,
-                "beta": BETA,
+                "k": prob.k,
+                "beta": prob.beta,
                 "arith": "fma",
-                "steps_per_launch": per_launch,
-                "lanes_per_chain": w.lanes,
-                "chains_per_lane": w.chains_per_lane,
-                "spec_width": w.spec_width,
+                "kernel_leg_steps_per_launch": per_launch,
+                "lanes_per_chain": lanes_k,
+                "chains_per_lane": cpl_k,
+                "spec_width": spec_k,
                 "parallelism": f"{total_chains} chains sharded over {world} GPU(s) ({args.scaling} scaling)",
                 "clock_settle_s": args.settle,
             },
@@ -463,19 +597,19 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC)",
                 "traffic_source": pmc_src,
-                "algorithmic_bytes": per_rank * per_launch * (D * ITEM[args.dtype] + 2 * (ITEM[args.dtype] + 8)),
+                "algorithmic_bytes": per_rank * per_launch * (prob.k * item + 2 * (item + 8)),
                 "hbm_GBps": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9,
                 "hbm_frac": None if traffic is None else traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "kernel_ms": kern_ms,
+                "kernel_time_source": "HIP events around the kernel leg's timed launches (extra.kernel_*); "
+                                      "tools/trace_summary.py restricts a rocprofv3 kernel trace to the same launches",
                 "flop_per_launch": flop,
                 "clock_GHz_pmc": None if pmc is None else pmc.get("effective_clock_GHz"),
                 "valu_issue_per_simd_cycle_pmc": None if pmc is None else pmc.get("valu_issue_per_simd_cycle"),
-                "mix_ceiling_frac": MIX_CEILING,
+                "mix_ceiling_frac": prob.mix_ceiling,
                 "note": "vector-ALU bound (FP64 pipe; packed FP32 for f32), no MFMA and no HBM traffic in the "
-                        "RK loop: algorithmic FLOP = 30*d*n per chain-step, issued as 20 VALU ops of which 10 "
-                        "FMA, so the op mix caps achieved/peak at mix_ceiling_frac (x clock/2.4 GHz); "
-                        "valu_issue_per_simd_cycle 0.25 = a wave64 op every 4 cycles = the pipe issuing every "
-                        "slot (traffic_source holds the PMC passes)",
+                        "forward map's time loop: algorithmic FLOP = 30*d*n per chain-step (cfg3/cfg5; Burgers "
+                        "30*N*n), on the kernel leg's launch time",
             },
             "cpu_baseline": cpu,
             "accept_rate": accept_rate,

@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 10
+#define IPMC_ABI_VERSION 11
 
 typedef enum {
   IPMC_OK = 0,
@@ -174,6 +174,10 @@ typedef struct ipmc_sweep {
                                  with n_s = n_steps / sample_every samples per chain the rows may not overlap:
                                  sample_stride >= (n_s-1)*sample_step_stride + k ([chain, sample, k]) or
                                  sample_step_stride >= (n_chains-1)*sample_stride + k ([sample, chain, k]) */
+  uint64_t accepts_step0;   /* (ABI 11) global pCN step at which the `accepts` counters started counting
+                               (MCMCSampler.run zeroes them at its first step; 0 = from step 0).  A speculative
+                               sweep's first round guesses accept mode when a chain accepted at least half of its
+                               steps since then (step0 - accepts_step0); results never depend on it. */
 } ipmc_sweep;
 
 /* pCN sweep: n_steps x (propose v, Φ(v) = ½‖(y−G(v))/γ‖², accept iff Φ(u)−Φ(v) > log r). */

@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -85,6 +85,7 @@ class IpmcSweep(C.Structure):
         ("prior_chol", C.c_void_p),
         ("sample_every", C.c_int64),
         ("sample_step_stride", C.c_int64),
+        ("accepts_step0", C.c_uint64),
     ]
 
 

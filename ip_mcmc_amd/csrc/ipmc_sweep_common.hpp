@@ -216,10 +216,12 @@ struct SpecGuess {
 #endif
 };
 // The prior at a launch's first round: the chain's accept counter over the
-// global steps before the launch (accept mode without any history).
+// steps it has counted before the launch (step0 - accepts_step0: a resumed or
+// continued run counts from its own first step, not from global step 0);
+// accept mode without any history.
 __device__ __forceinline__ bool spec_accept_prior(const ipmc_sweep& s, int64_t chain) {
-  if (!s.accepts || s.step0 == 0) return true;
-  return (uint64_t)(2 * s.accepts[chain]) >= s.step0;
+  if (!s.accepts || s.step0 <= s.accepts_step0) return true;
+  return (uint64_t)(2 * s.accepts[chain]) >= s.step0 - s.accepts_step0;
 }
 
 struct SpecRound {

@@ -255,6 +255,7 @@ class MCMCSampler:
         if const_beta:
             sw.beta, sw.contraction = plan.proposer.device_step()
         sw.seed = rng.seed
+        sw.accepts_step0 = rng.step  # the accept counters start at this run's first step
         # the accept potential of the starting states: Φ(u), or I(u) for StandardRWAccepter
         state_dtype = "float64" if td == torch.float64 else "float32"
         if resume and u_0.phi.shape[0] != n_chains:

@@ -9,6 +9,9 @@ collective is the final gather of per-chain results to every rank
 xGMI on MI355X, "gloo" on CPU), followed by a host reduction in fixed global
 chain order, so posterior means are also bitwise independent of P.
 """
+import os
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -46,12 +49,157 @@ def ordered_mean(x, block=1 << 16):
     running sum ((0 + row_0) + row_1) + ... is np.cumsum along the chain axis
     (a strictly sequential accumulate), taken in blocks of rows so that the
     2^20-chain case needs no full-size temporary."""
-    import numpy as np
-
     a = x.detach().double().cpu().numpy() if hasattr(x, "detach") else np.asarray(x, dtype=np.float64)
-    acc = np.zeros(a.shape[1:], dtype=np.float64)
+    return _seq_sum(a, np.zeros(a.shape[1:], dtype=np.float64), block) / a.shape[0]
+
+
+def _seq_sum(a, acc, block=1 << 16):
+    """acc + a[0] + a[1] + ... strictly in row order (blocked np.cumsum)."""
     for i in range(0, a.shape[0], block):
         blk = a[i : i + block].copy()
         blk[0] = acc + blk[0]
         acc = np.cumsum(blk, axis=0)[-1]
-    return acc / a.shape[0]
+    return acc
+
+
+def ordered_sum_sharded(local, group=None, block=1 << 16):
+    """The sequential sum ((0 + row_0) + row_1) + ... over chains in global
+    order when the rows are spread over the ranks in rank order: rank r
+    continues rank r-1's running sum (one small message per rank boundary,
+    send/recv), and the last rank's total is broadcast to every rank.
+    Bit-identical to ordered_mean's sum over the gathered rows, without
+    gathering them (config 5's per-chain sums are 4 GB)."""
+    rank, world = world_info(group)
+    a = np.asarray(local, dtype=np.float64)
+    acc = np.zeros(a.shape[1:], dtype=np.float64)
+    if world == 1:
+        return _seq_sum(a, acc, block)
+    dev = _comm_device(group)
+    glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+    if rank > 0:
+        t = torch.empty(acc.shape, dtype=torch.float64, device=dev)
+        dist.recv(t, src=glob(rank - 1), group=group)
+        acc = t.cpu().numpy()
+    acc = _seq_sum(a, acc, block)
+    if rank < world - 1:
+        dist.send(torch.from_numpy(acc).to(dev), dst=glob(rank + 1), group=group)
+    t = torch.from_numpy(np.ascontiguousarray(acc)).to(dev)
+    dist.broadcast(t, src=glob(world - 1), group=group)
+    return t.cpu().numpy()
+
+
+def world_info(group=None):
+    """(rank, world size) of this process: the initialised process group, else
+    RANK / WORLD_SIZE from the environment (torchrun), else (0, 1)."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def _comm_device(group):
+    """Where a collective's tensors live: the rank's GPU for RCCL ("nccl"),
+    host memory for gloo."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200, keep="moments", group=None,
+                sample_file=None, gather="all"):
+    """MCMCSampler.run over the chains of every rank of a node, one process per GPU.
+
+    make_sampler(chain_offset=...) builds this rank's sampler (the same
+    proposer / accepter / potential / rng seed on every rank; the sampler's
+    chain_offset must be the one passed).  u_0 (C_total, k) is the full
+    ensemble's starting states on every rank (an array, e.g. a memory-mapped
+    .npy; each rank reads only its block of rows).  Rank r runs the
+    chains chain_range(C_total, r, P) -- global ids, so every chain's
+    trajectory is the one-process run's bit for bit -- and the per-chain
+    results of all ranks are gathered by one all_gather_into_tensor (RCCL over
+    xGMI with backend "nccl", gloo on CPU) into global chain order.
+
+    Returns a dict on every rank:
+      "u", "phi", "accepts"   the final chain states (C_total, k), Φ, accept counts
+      keep="moments": "sum_u", "sum_u2" (C_total, k) and "n", plus "mean"
+                     (the posterior-mean estimate: the per-chain time averages
+                     averaged over chains in fixed global order, ordered_mean --
+                     bit-identical for any number of ranks)
+      keep="samples": "samples" (C_total, n_samples, k); with sample_file each
+                     rank streams its own block to f"{sample_file}.rank{r}.npy"
+                     and nothing is gathered but the state
+      keep="last":   "last" (C_total, k)
+      "rank", "world", "chain_range", "local" (this rank's own run() result),
+      "sampler" (this rank's sampler, state included), "run_seconds" (this
+      rank's run()), "gather_seconds".
+    gather="mean" (keep="moments" only) gathers just Φ and the accept counts
+    and forms "mean" by the rank-sequential ordered_sum_sharded, for ensembles
+    whose per-chain arrays are too large to copy to every rank (config 5:
+    2^20 chains x 256); "u", "sum_u", "sum_u2" are then this rank's rows only.
+    With one rank (no process group) it is a plain run()."""
+    import time
+
+    rank, world = world_info(group)
+    if world > 1 and not (dist.is_available() and dist.is_initialized()):
+        raise RuntimeError("run_sharded with WORLD_SIZE > 1 needs an initialised process group "
+                           "(torch.distributed.init_process_group('nccl') on the GPUs, 'gloo' on CPU)")
+    if gather not in ("all", "mean"):
+        raise ValueError("gather must be 'all' or 'mean'")
+    if gather == "mean" and keep != "moments":
+        raise ValueError("gather='mean' needs keep='moments'")
+    if len(np.shape(u_0)) != 2:
+        raise ValueError("run_sharded needs u_0 of shape (chains, k)")
+    n_total = int(np.shape(u_0)[0])
+    lo, hi = chain_range(n_total, rank, world)
+    sampler = make_sampler(chain_offset=lo)
+    if sampler.chain_offset != lo:
+        raise ValueError(f"make_sampler must build the sampler with chain_offset={lo}, got {sampler.chain_offset}")
+    local_u0 = np.asarray(u_0[lo:hi], dtype=np.float64)
+    sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
+    t0 = time.perf_counter()
+    res = sampler.run(local_u0, n_samples, burn_in=burn_in, sample_interval=sample_interval, keep=keep,
+                      sample_file=sf)
+    run_s = time.perf_counter() - t0
+    st = sampler.state
+    k = local_u0.shape[1]
+    cols = [np.asarray(st.u, dtype=np.float64).reshape(hi - lo, k),
+            np.asarray(st.phi, dtype=np.float64).reshape(hi - lo, 1),
+            np.asarray(st.accepts, dtype=np.float64).reshape(hi - lo, 1)]  # counts < 2^53: exact
+    if gather == "mean":
+        t1 = time.perf_counter()
+        small = np.concatenate(cols[1:], axis=1)
+        if world > 1:
+            small = gather_chains(torch.from_numpy(np.ascontiguousarray(small)).to(_comm_device(group)), n_total,
+                                  group).cpu().numpy()
+        n = max(1, res["n"])
+        mean = ordered_sum_sharded(res["sum_u"].reshape(hi - lo, k) / n, group) / n_total
+        return {"u": cols[0], "phi": small[:, 0], "accepts": small[:, 1].astype(np.int64), "sum_u": res["sum_u"],
+                "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
+                "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
+                "gather_seconds": time.perf_counter() - t1}
+    if keep == "moments":
+        cols += [res["sum_u"].reshape(hi - lo, k), res["sum_u2"].reshape(hi - lo, k)]
+    elif keep == "samples" and sf is None:
+        cols.append(np.asarray(res, dtype=np.float64).reshape(hi - lo, -1))
+    elif keep == "last":
+        cols.append(np.asarray(res, dtype=np.float64).reshape(hi - lo, k))
+    packed = np.concatenate(cols, axis=1) if hi > lo else np.zeros((0, sum(c.shape[1] for c in cols)))
+    t1 = time.perf_counter()
+    if world > 1:
+        dev = _comm_device(group)
+        full = gather_chains(torch.from_numpy(np.ascontiguousarray(packed)).to(dev), n_total, group)
+        full = full.cpu().numpy()
+    else:
+        full = packed
+    gather_s = time.perf_counter() - t1
+    out = {"u": full[:, :k], "phi": full[:, k], "accepts": full[:, k + 1].astype(np.int64), "rank": rank,
+           "world": world, "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
+           "gather_seconds": gather_s}
+    rest = full[:, k + 2:]
+    if keep == "moments":
+        out["sum_u"], out["sum_u2"], out["n"] = rest[:, :k], rest[:, k:2 * k], res["n"]
+        out["mean"] = ordered_mean(out["sum_u"] / max(1, res["n"]))
+    elif keep == "samples" and sf is None:
+        out["samples"] = rest.reshape(n_total, -1, k)
+    elif keep == "last":
+        out["last"] = rest
+    return out

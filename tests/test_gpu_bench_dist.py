@@ -3,7 +3,9 @@ the final gather, rank-0 JSON line) rehearsed with 2 ranks on the one-GPU box:
 both ranks on cuda:0 and gloo for the collectives (RCCL needs one GPU per rank;
 the driver's 8-GPU runs use it).  Started both ways: under an external
 torch.distributed.run (the driver's form) and as plain `python bench.py --gpus 2`,
-which launches the ranks itself (strong scaling on the metric's 65 536 chains)."""
+which launches the ranks itself (strong scaling on the metric's 65 536 chains),
+and the config-5 workload (2^20 chains over the ranks, f64, through
+shard.run_sharded with the rank-sequential posterior mean)."""
 import json
 import os
 import socket
@@ -29,7 +31,7 @@ def test_bench_two_ranks_rehearsal():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--chains", "4096", "--scaling", "weak", "--no-cpu", "--no-extra",
-           "--dist-backend", "gloo", "--share-device"]
+           "--no-configs", "--dist-backend", "gloo", "--share-device"]
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -44,14 +46,35 @@ def test_bench_two_ranks_rehearsal():
 def test_bench_gpus_2_launches_its_own_ranks():
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--no-cpu", "--dist-backend", "gloo", "--share-device"]
-    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=400)
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["total_chains"] == 65536 and line["config"]["chains_per_gpu"] == 32768
-    assert line["final_gather"]["rows"] == 65536
+    assert line["final_gather"]["rows"] == 65536 and line["final_gather"]["inside_timed_region"]
     ex = line["extra"]
     assert ex["weak_scaling"]["total_chains"] == 131072 and ex["weak_scaling"]["pcn_steps_per_s"] > 0
-    assert ex["reference_arith_pcn_steps_per_s"] > 0 and ex["run_e2e_pcn_steps_per_s"] > 0
+    assert ex["reference_arith_kernel_pcn_steps_per_s"] > 0 and ex["run_e2e_samples"]["pcn_steps_per_s"] > 0
+    # value is the end-to-end run; the kernel leg is beside it
+    assert line["value"] == ex["run_e2e_moments"]["pcn_steps_per_s"] and ex["kernel_pcn_steps_per_s"] > 0
+    assert abs(line["ms_per_step"] * line["steps"] / 1e3 - ex["run_e2e_moments"]["wall_s"]) < 1e-9
+    assert ex["configs"]["cfg4"]["f64"]["total_chains"] == 16384
+    assert ex["configs"]["cfg5"]["f64"]["total_chains"] == 1 << 20 and ex["configs"]["cfg5"]["f32"]["pcn_steps_per_s"] > 0
+
+
+def test_bench_cfg5_workload_two_ranks():
+    """`bench.py --gpus 2 --workload cfg5`: one line for BASELINE config 5 at its
+    full ensemble (2^20 chains, 524 288 per rank)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--workload", "cfg5", "--steps", "2",
+           "--warmup", "1", "--no-cpu", "--dist-backend", "gloo", "--share-device"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["config"]["workload"] == "lorenz96_d256_rk4_10000_pcn"
+    assert line["config"]["total_chains"] == 1 << 20 and line["config"]["chains_per_gpu"] == 1 << 19
+    assert line["final_gather"]["mode"] == "mean" and line["final_gather"]["rows"] == 1 << 20
+    assert line["value"] > 0

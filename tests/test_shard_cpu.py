@@ -116,3 +116,79 @@ def test_ordered_mean_equals_the_sequential_loop():
     assert np.array_equal(ordered_mean(torch.from_numpy(a), block=4096), want)
     assert np.array_equal(ordered_mean(a[:1000], block=7), ordered_mean(torch.from_numpy(a[:1000])))
     assert np.array_equal(ordered_mean(a[:5], block=3), np.cumsum(a[:5], axis=0)[-1] / 5)
+
+
+# ---------------------------------------------- shard.run_sharded (product)
+def _lin_sampler_factory():
+    """A host-tier composition (a Python closure G, the reference's config-1
+    form) that runs on CPU ranks: the host step draws from libipmc_host.so."""
+    from ip_mcmc_amd import (ConstSteppCNProposer, CountedAccepter, EvolutionPotential, GaussianDistribution,
+                             MCMCSampler, PhiloxRNG, pCNAccepter)
+
+    g = np.array([3.0, 1.0, 4.0, 1.0])
+    y = np.dot(g, [2.0, 7.0, 1.0, 8.0]) + 0.5 * 0.3
+
+    def make(chain_offset=0):
+        pot = EvolutionPotential(lambda u: np.dot(g, u), y, GaussianDistribution(0, 0.25))
+        return MCMCSampler(ConstSteppCNProposer(0.5, GaussianDistribution(np.zeros(4), np.eye(4))),
+                           CountedAccepter(pCNAccepter(pot)), PhiloxRNG(21), chain_offset=chain_offset)
+
+    return make
+
+
+def _sharded_worker(rank, world, port, out_path, keep, gather="all"):
+    import sys
+
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import run_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(C_TOTAL, 4))
+    res = run_sharded(_lin_sampler_factory(), u0, n_samples=6, burn_in=9, sample_interval=4, keep=keep,
+                      gather=gather)
+    assert res["world"] == world and res["sampler"].last_path == "host"
+    if rank == 1:  # every rank holds the gathered result
+        body = {k: v for k, v in res.items() if isinstance(v, np.ndarray)}
+        np.savez(out_path, **body)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("keep", ["moments", "samples"])
+def test_run_sharded_equals_one_process(tmp_path, keep):
+    """run_sharded over gloo, world 3, = one process's run(): states, Φ, accept
+    counts, sums or samples and the ordered posterior mean, bit for bit."""
+    from ip_mcmc_amd.shard import run_sharded
+
+    out = str(tmp_path / "s.npz")
+    mp.start_processes(_sharded_worker, args=(3, _free_port(), out, keep), nprocs=3, start_method="spawn")
+    got = np.load(out)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(C_TOTAL, 4))
+    one = run_sharded(_lin_sampler_factory(), u0, n_samples=6, burn_in=9, sample_interval=4, keep=keep)
+    assert one["world"] == 1
+    keys = ["u", "phi", "accepts"] + (["sum_u", "sum_u2", "mean"] if keep == "moments" else ["samples"])
+    for key in keys:
+        assert np.array_equal(got[key], one[key]), key
+    assert one["accepts"].sum() > 0
+    if keep == "moments":
+        want = _lin_sampler_factory()(0).run(u0, n_samples=6, burn_in=9, sample_interval=4, keep="moments")
+        np.testing.assert_array_equal(one["sum_u"], want["sum_u"])
+
+
+def test_run_sharded_mean_by_rank_sequential_sum(tmp_path):
+    """gather='mean': no per-chain sums leave their rank, yet the posterior
+    mean (a rank-sequential ordered sum) and the gathered Φ / accept counts
+    equal the one-process run's bit for bit (gloo, world 3)."""
+    from ip_mcmc_amd.shard import run_sharded
+
+    out = str(tmp_path / "m.npz")
+    mp.start_processes(_sharded_worker, args=(3, _free_port(), out, "moments", "mean"), nprocs=3,
+                       start_method="spawn")
+    got = np.load(out)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(C_TOTAL, 4))
+    one = run_sharded(_lin_sampler_factory(), u0, n_samples=6, burn_in=9, sample_interval=4, keep="moments")
+    for key in ("mean", "phi", "accepts"):
+        assert np.array_equal(got[key], one[key]), key
+    assert got["sum_u"].shape[0] == 12  # rank 1's own block of chain_range(37, 1, 3)

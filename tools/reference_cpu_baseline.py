@@ -6,7 +6,8 @@ GaussianDistribution, with G = classical RK4 (dt 0.005, 2000 steps, time
 average) over the reference's own Lorenz96 RHS object (lorenz.py:13-111, J=0,
 d=40) -- the reference has no RK4 driver, so this is the smallest wrapper that
 makes its code run config 3.  One chain per process, P processes; stdout of
-the sampler suppressed.  Writes profiles/r1/reference_cpu_cfg3.json, which
+the sampler suppressed; --steps 60 keeps every process busy for > 30 s (1.7
+pCN steps/s per core).  Writes profiles/r4/reference_cpu_cfg3.json, which
 bench.py reports next to its own cpu_baseline (clearly labelled: measured
 here, not on the GPU box).
 
@@ -126,7 +127,7 @@ def config1(n_samples):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=len(os.sched_getaffinity(0)))
-    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--samples", type=int, default=500)
     args = ap.parse_args()
@@ -146,12 +147,15 @@ def main():
         "per_core": float(sum(per_proc) / args.procs),
         "sample": f"{args.procs} processes x 1 chain x {args.steps} pCN steps of config 3 (d=40, 2000 RK4 "
                   f"steps, f64) through the reference MCMCSampler/pCNAccepter/EvolutionPotential with the "
-                  f"reference Lorenz96 RHS; 2 G evaluations per step (Φ(u) recomputed, accepter.py:122)",
+                  f"reference Lorenz96 RHS; 2 G evaluations per step (Φ(u) recomputed, accepter.py:122); "
+                  f"{min(times):.1f}-{max(times):.1f} s of sampling per process",
+        "seconds_per_process": [float(t) for t in times],
         "host": platform.processor() or platform.machine(),
         "measured_on": "build container (the reference does not exist on the GPU box)",
         "wall_s": wall,
     }
-    out = os.path.join(REPO, "profiles", "r1", "reference_cpu_cfg3.json")
+    out = os.path.join(REPO, "profiles", "r4", "reference_cpu_cfg3.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec))
