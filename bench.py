@@ -427,6 +427,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the short cfg4 / cfg5 runs in extra.configs")
+    ap.add_argument("--pmc-file", default=None,
+                    help="a tools/pmc_summarize.py record of this box's PMC passes for roofline.traffic (default: the "
+                         "newest committed profiles/r*/pmc_l96_<dtype>.json of the same kernel and layout)")
+    ap.add_argument("--kernel-only", action="store_true",
+                    help="profiling runs: the kernel leg only (no end-to-end leg, extras or CPU baseline), so a "
+                         "rocprofv3 trace or PMC pass holds the timed sweep launches and nothing else; the line's "
+                         "value is then the kernel leg's rate (marked kernel_only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the product path) or gloo (rehearsal of the N-rank logic)")
     ap.add_argument("--share-device", action="store_true",
@@ -477,11 +484,18 @@ def main():
     log(f"kernel leg: {el_k:.3f} s, kernel {kern_ms:.3f} ms/launch, {kernel_rate / 1e6:.2f} M steps/s")
     lanes_k, cpl_k, spec_k = w.lanes, w.chains_per_lane, w.spec_width
     del w
+    if args.kernel_only:
+        args.no_extra = args.no_configs = args.no_cpu = True
 
     # 2. value: MCMCSampler.run end to end through shard.run_sharded
     gather_mode = "mean" if total_chains * prob.k > (1 << 26) else "all"
-    log(f"end-to-end leg: run_sharded({total_chains} chains, {steps} steps, keep='moments', gather={gather_mode})")
-    e2e, res = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode)
+    if args.kernel_only:
+        e2e = {"pcn_steps_per_s": kernel_rate, "wall_s": el_k, "ms_per_step": el_k / steps * 1e3,
+               "accept_rate": None, "gather_ms": 0.0, "kernel_only": True}
+        res = {"phi": np.zeros(0), "mean": np.zeros(0), "accepts": np.zeros(0)}
+    else:
+        log(f"end-to-end leg: run_sharded({total_chains} chains, {steps} steps, keep='moments', gather={gather_mode})")
+        e2e, res = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode)
     value = e2e["pcn_steps_per_s"]
     log(f"end-to-end: {e2e['wall_s']:.3f} s, {value / 1e6:.2f} M steps/s")
     gather = {"ms": e2e["gather_ms"], "mode": gather_mode,
@@ -489,7 +503,7 @@ def main():
               "collective": (f"all_gather_into_tensor ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
                              + (" + rank-sequential ordered sum (send/recv)" if gather_mode == "mean" else "")
                              if world > 1 else "none (one rank)"),
-              "rows": int(res["phi"].shape[0]), "inside_timed_region": True}
+              "rows": int(res["phi"].shape[0]), "inside_timed_region": not args.kernel_only}
     assert np.isfinite(res["phi"]).all() and np.isfinite(res["mean"]).all()
     accept_rate = e2e["accept_rate"]
     del res
@@ -543,6 +557,8 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
     is_l96_40 = args.workload == "cfg3"
     pmc, pmc_src = pmc_record(args.dtype, per_rank, lanes_k) if (per_launch == 1 and is_l96_40) else (None, None)
+    if args.pmc_file:
+        pmc, pmc_src = json.load(open(args.pmc_file)), os.path.relpath(os.path.abspath(args.pmc_file), REPO)
     traffic = None if pmc is None else pmc["hbm_bytes_per_launch"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -567,6 +583,7 @@ def main():
             "warmup": warmup,
             "ms_per_step": e2e["ms_per_step"],
             "higher_is_better": True,
+            "kernel_only": bool(args.kernel_only),
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,

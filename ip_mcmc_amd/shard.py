@@ -176,30 +176,36 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
                 "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
                 "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
                 "gather_seconds": time.perf_counter() - t1}
-    if keep == "moments":
-        cols += [res["sum_u"].reshape(hi - lo, k), res["sum_u2"].reshape(hi - lo, k)]
-    elif keep == "samples" and sf is None:
-        cols.append(np.asarray(res, dtype=np.float64).reshape(hi - lo, -1))
-    elif keep == "last":
-        cols.append(np.asarray(res, dtype=np.float64).reshape(hi - lo, k))
-    packed = np.concatenate(cols, axis=1) if hi > lo else np.zeros((0, sum(c.shape[1] for c in cols)))
     t1 = time.perf_counter()
-    if world > 1:
-        dev = _comm_device(group)
-        full = gather_chains(torch.from_numpy(np.ascontiguousarray(packed)).to(dev), n_total, group)
-        full = full.cpu().numpy()
+    out = {"rank": rank, "world": world, "chain_range": (lo, hi), "local": res, "sampler": sampler,
+           "run_seconds": run_s}
+    if world == 1:  # nothing to gather: this process's arrays are the result
+        out.update(u=cols[0], phi=cols[1][:, 0], accepts=np.asarray(st.accepts, dtype=np.int64))
+        if keep == "moments":
+            out.update(sum_u=res["sum_u"].reshape(hi - lo, k), sum_u2=res["sum_u2"].reshape(hi - lo, k), n=res["n"])
+        elif keep == "samples" and sf is None:
+            out["samples"] = np.asarray(res, dtype=np.float64).reshape(hi - lo, -1, k)
+        elif keep == "last":
+            out["last"] = np.asarray(res, dtype=np.float64).reshape(hi - lo, k)
     else:
-        full = packed
-    gather_s = time.perf_counter() - t1
-    out = {"u": full[:, :k], "phi": full[:, k], "accepts": full[:, k + 1].astype(np.int64), "rank": rank,
-           "world": world, "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
-           "gather_seconds": gather_s}
-    rest = full[:, k + 2:]
+        if keep == "moments":
+            cols += [res["sum_u"].reshape(hi - lo, k), res["sum_u2"].reshape(hi - lo, k)]
+        elif keep == "samples" and sf is None:
+            cols.append(np.asarray(res, dtype=np.float64).reshape(hi - lo, -1))
+        elif keep == "last":
+            cols.append(np.asarray(res, dtype=np.float64).reshape(hi - lo, k))
+        packed = np.concatenate(cols, axis=1) if hi > lo else np.zeros((0, sum(c.shape[1] for c in cols)))
+        full = gather_chains(torch.from_numpy(np.ascontiguousarray(packed)).to(_comm_device(group)), n_total,
+                             group).cpu().numpy()
+        out.update(u=full[:, :k], phi=full[:, k], accepts=full[:, k + 1].astype(np.int64))
+        rest = full[:, k + 2:]
+        if keep == "moments":
+            out.update(sum_u=rest[:, :k], sum_u2=rest[:, k:2 * k], n=res["n"])
+        elif keep == "samples" and sf is None:
+            out["samples"] = rest.reshape(n_total, -1, k)
+        elif keep == "last":
+            out["last"] = rest
     if keep == "moments":
-        out["sum_u"], out["sum_u2"], out["n"] = rest[:, :k], rest[:, k:2 * k], res["n"]
         out["mean"] = ordered_mean(out["sum_u"] / max(1, res["n"]))
-    elif keep == "samples" and sf is None:
-        out["samples"] = rest.reshape(n_total, -1, k)
-    elif keep == "last":
-        out["last"] = rest
+    out["gather_seconds"] = time.perf_counter() - t1
     return out

@@ -1,16 +1,24 @@
-"""The benched arithmetic against the reference's at the headline shape.
+"""The benched arithmetic against the reference's, on a stationary posterior at
+the headline shape.
 
 bench.py times the FMA forward map; the chains pinned bit for bit to the
-reference fixtures run REFERENCE arith (no FMA, lorenz.py:77-81's order).  At
-65 536 chains x d=40 x 2 000 RK4 steps in f64 (tools/arith_agreement.py,
-profiles/r3/arith_agreement.jsonl) this states how far apart they are:
+reference fixtures run REFERENCE arith (no FMA, lorenz.py:77-81's order).
+tools/posterior_agreement.py (`arith`) runs both on the forcing-field
+posterior at the headline shape (Lorenz-96 d=40, 2 000 RK4 steps, f64) with
+the reference's own noise recipe (lorenz_mcmc.py:100-112, r = 0.5), from
+independent prior draws u_0 with independent Philox seeds, long enough to
+reach stationarity; it discards the burn-in diagnostics.burn_in_lengths finds
+and estimates Monte-Carlo standard errors by batch means.  The stated
+tolerance:
 
-* paired (same u_0, same Philox draws): at least PAIRED_MIN of the chains make
-  identical accept decisions over the whole run (identical accept counts);
-* independent seeds: the posterior-mean estimates of every one of the 40
-  components agree within Z_MAX Monte-Carlo standard errors (family-wise
-  false-alarm probability ~0.25 % at Z_MAX = 4 over 40 components), and the
-  mean z² is below 1 + 3·sqrt(2/40) (a chi-square bound on all 40 at once).
+* the chains reach stationarity: split-R̂ < RHAT_MAX and the first and second
+  halves of the post-burn-in run agree (|z| < Z_MAX) for every component;
+* the posterior means of the two arithmetics agree: max_i |z_i| < Z_MAX
+  (family-wise false alarm ~0.25 % over 40 components) and both mean z² and
+  the whitened T²/d lie in 1 ± 3.5·sqrt(2/d) (two-sided: a statistic far below
+  1 means the standard errors are mis-calibrated);
+* paired (same u_0 and draws): at least PAIRED_MIN of the chains make the same
+  accept decisions over the whole run.
 """
 import os
 import sys
@@ -22,22 +30,32 @@ pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
+D = 40
 PAIRED_MIN = 0.99
 Z_MAX = 4.0
-MEAN_Z2_MAX = 1 + 3 * np.sqrt(2 / 40)
+BAND = 3.5 * np.sqrt(2 / D)
+RHAT_MAX = 1.1
+# (chains, blocks, steps per block, beta): 2 400 pCN steps per chain
+RUN = (8192, 48, 50, 0.2)
 
 
-@pytest.mark.parametrize("beta,start", [(0.2, "zero"), (0.02, "posterior")])
-def test_fma_and_reference_arith_agree_at_the_headline_shape(beta, start):
+def test_fma_and_reference_posteriors_agree_at_the_headline_shape():
     import torch
 
-    import arith_agreement as A
+    import posterior_agreement as PA
 
     assert torch.cuda.is_available()
-    r = A.measure(beta, 40, chains=65536, start=start)
+    chains, n_seg, seg_len, beta = RUN
+    r = PA.measure("arith", chains, n_seg, seg_len, beta)
     print(r)
-    assert r["chains"] == 65536
+    assert r["d"] == D and r["rk4_steps"] == 2000 and r["chains"] == chains
+    assert "burn_in_capped_from" not in r, r  # the burn-in ends inside the run
+    for arm in ("fma_float64", "reference_float64"):
+        a = r[arm]
+        assert 0.02 < a["accept_rate"] < 0.98, a
+        assert a["rhat_max"] < RHAT_MAX, a
+        assert a["half_z_max"] < Z_MAX, a
+    assert r["max_z"] < Z_MAX, r
+    assert abs(r["mean_z2"] - 1) < BAND, r
+    assert abs(r["t2_over_d"] - 1) < BAND, r
     assert r["paired_identical_accept_counts"] >= PAIRED_MIN, r
-    assert r["indep_max_z"] < Z_MAX, r
-    assert r["indep_mean_z2"] < MEAN_Z2_MAX, r
-    assert r["accept_rate_fma"] > 0 and r["accept_rate_ref"] > 0

@@ -95,11 +95,14 @@ def make(cfg):
         return op, 16384, 0.5, np.sqrt([10.0, 1.0, 10.0]), 45 * 396 * 2000, 0.5
     if cfg.startswith("l96"):
         # the headline problem with few chains (the reference runs one): speculation
-        # territory; "l96d80x16384": another dimension
-        mt = re.fullmatch(r"l96(?:d(\d+))?x(\d+)", cfg)
-        d = int(mt.group(1) or 40)
+        # territory; "l96d80x16384": another dimension; "l96mx64": the mixing
+        # posterior of tools/posterior_agreement.py (gamma = 0.5 sd(X) = 1.8,
+        # the reference's noise recipe) instead of gamma = 0.1, whose chains
+        # accept almost nothing -- the best case for a speculative sweep
+        mt = re.fullmatch(r"l96(m?)(?:d(\d+))?x(\d+)", cfg)
+        d = int(mt.group(2) or 40)
         op = Lorenz96Operator(d, 8.0, dt=0.005, n_steps=2000)
-        return op, int(mt.group(2)), 0.2, np.ones(d), 30 * d * 2000, 0.1
+        return op, int(mt.group(3)), 0.2, np.ones(d), 30 * d * 2000, (1.8 if mt.group(1) else 0.1)
     raise SystemExit(f"unknown config {cfg}")
 
 

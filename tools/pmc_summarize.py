@@ -1,7 +1,10 @@
 """Summarise rocprofv3 PMC passes of the headline sweep kernel into
 profiles/<round>/pmc_l96_<dtype>.json (read by bench.py for roofline.traffic).
 
-  python tools/pmc_summarize.py <dir with fetch/write/sq csv> <dtype> <chains> <out.json>
+  python tools/pmc_summarize.py <dir with fetch/write/sq csv> <dtype> <chains> <out.json> [first]
+
+`first`: only the first N dispatches of the sweep kernel in each pass (start
+order) -- bench.py's kernel leg when the run also has later legs.
 
 Inputs: the three separate passes (FETCH_SIZE; WRITE_SIZE; SQ_WAVES,
 SQ_INSTS_VALU, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE), each
@@ -27,13 +30,19 @@ def rows(path):
         yield from csv.DictReader(f)
 
 
-def per_dispatch(files, match):
-    """{counter: [value per dispatch]} for kernels whose name contains `match`."""
+def per_dispatch(files, match, first=None):
+    """{counter: [value per dispatch]} for kernels whose name contains `match`
+    (the first `first` dispatches of each file in start order, if given)."""
     acc = defaultdict(lambda: defaultdict(float))
     meta = {}
     for path in files:
-        for r in rows(path):
-            if match not in r["Kernel_Name"]:
+        rs = [r for r in rows(path) if match in r["Kernel_Name"]]
+        keep = None
+        if first:
+            starts = sorted({(int(r["Start_Timestamp"]), r["Dispatch_Id"]) for r in rs})
+            keep = {d for _, d in starts[:first]}
+        for r in rs:
+            if keep is not None and r["Dispatch_Id"] not in keep:
                 continue
             key = (path, r["Dispatch_Id"])
             acc[r["Counter_Name"]][key] += float(r["Counter_Value"])
@@ -43,8 +52,9 @@ def per_dispatch(files, match):
 
 def main():
     src, dtype, chains, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    first = int(sys.argv[5]) if len(sys.argv) > 5 else None
     files = sorted(glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True))
-    vals, meta = per_dispatch(files, "l96_sweep")
+    vals, meta = per_dispatch(files, "l96_sweep", first)
     mean = lambda xs: sum(xs) / len(xs)
     d, k_bytes = 40, 8 if dtype == "f64" else 4
     fetch, write = mean(vals["FETCH_SIZE"]), mean(vals["WRITE_SIZE"])
