@@ -60,6 +60,77 @@ __device__ __forceinline__ void l63_forward(T sg, T rh, T bb, const T* __restric
   for (int i = 0; i < 6; ++i) g[i] = ob[i] / nn;
 }
 
+#ifndef IPMC_L63_PK  // experiments (tools/build_variant.sh): 0 = the scalar fp32 loop
+#define IPMC_L63_PK 1
+#endif
+
+// fp32: the same RK4 with components (x, y) held as one f32x2 pair P and z
+// scalar.  Everything elementwise over the components -- the stage inputs,
+// the k-sum, the update and the moments -- is one v_pk_*_f32 for x and y
+// (per-element IEEE operations, so the bits of l63_forward<float>); only the
+// right-hand side, whose three rates have different formulas, stays scalar.
+// 51 -> 42 VALU ops per RK4 step: config 2 runs one wave per SIMD (4 096
+// chains x 16 speculative slots), where a single wave's issue rate, not its
+// dependent chain, bounds a round, so fewer instructions are
+// a shorter round.
+template <bool FM>
+__device__ __forceinline__ void l63_rhs_pk(float sg, float rh, float bb, f32x2 p, float z, f32x2& kp, float& kz) {
+  const float s[3] = {p.x, p.y, z};
+  float o[3];
+  l63_rhs<float, FM>(sg, rh, bb, s, o);
+  kp = f32x2{o[0], o[1]};
+  kz = o[2];
+}
+
+template <bool FM>
+__device__ __forceinline__ void l63_forward_pk(float sg, float rh, float bb, const float* __restrict__ x0, float h,
+                                               int nsteps, float (&g)[6]) {
+  const float h2 = h * 0.5f, h6 = h / 6.0f;
+  const f32x2 H2 = {h2, h2}, H = {h, h}, H6 = {h6, h6}, TWO = {2.0f, 2.0f};
+  f32x2 P = {x0[0], x0[1]};
+  float z = x0[2];
+  f32x2 obP = {0.0f, 0.0f}, ob2P = {0.0f, 0.0f};
+  float obz = 0.0f, ob2z = 0.0f;
+  for (int n = 0; n < nsteps; ++n) {
+    f32x2 k1, k2, k3, k4, xs;
+    float k1z, k2z, k3z, k4z, xsz;
+    l63_rhs_pk<FM>(sg, rh, bb, P, z, k1, k1z);
+    xs = madd<FM>(H2, k1, P);
+    xsz = madd<FM>(h2, k1z, z);
+    l63_rhs_pk<FM>(sg, rh, bb, xs, xsz, k2, k2z);
+    xs = madd<FM>(H2, k2, P);
+    xsz = madd<FM>(h2, k2z, z);
+    l63_rhs_pk<FM>(sg, rh, bb, xs, xsz, k3, k3z);
+    xs = madd<FM>(H, k3, P);
+    xsz = madd<FM>(h, k3z, z);
+    l63_rhs_pk<FM>(sg, rh, bb, xs, xsz, k4, k4z);
+    // l63_forward's ((k1 + 2 k2) + 2 k3) + k4 in the same per-element operations
+    const f32x2 a = FM ? madd<true>(TWO, k3, madd<true>(TWO, k2, k1)) + k4 : ((k1 + TWO * k2) + TWO * k3) + k4;
+    const float az = FM ? madd<true>(2.0f, k3z, madd<true>(2.0f, k2z, k1z)) + k4z
+                        : ((k1z + 2.0f * k2z) + 2.0f * k3z) + k4z;
+    P = madd<FM>(H6, a, P);
+    z = madd<FM>(h6, az, z);
+    obP = obP + P;
+    obz = obz + z;
+    ob2P = madd<FM>(P, P, ob2P);
+    ob2z = madd<FM>(z, z, ob2z);
+  }
+  const float nn = (float)nsteps;
+  g[0] = obP.x / nn;
+  g[1] = obP.y / nn;
+  g[2] = obz / nn;
+  g[3] = ob2P.x / nn;
+  g[4] = ob2P.y / nn;
+  g[5] = ob2z / nn;
+}
+
+// The forward map of small_potential / small_eval_kernel: packed components for fp32.
+template <typename T, bool FM>
+__device__ __forceinline__ void l63_G(T sg, T rh, T bb, const T* __restrict__ x0, T h, int nsteps, T (&g)[6]) {
+  if constexpr (sizeof(T) == 4 && IPMC_L63_PK) l63_forward_pk<FM>(sg, rh, bb, x0, h, nsteps, g);
+  else l63_forward<T, FM>(sg, rh, bb, x0, h, nsteps, g);
+}
+
 // Φ for the lane's chain; v is read from the LDS park (column `col`).
 template <typename T, int MODEL, bool FM>
 __device__ __forceinline__ T small_potential(const ipmc_model& m, const T* __restrict__ v, int vstride,
@@ -68,8 +139,8 @@ __device__ __forceinline__ T small_potential(const ipmc_model& m, const T* __res
   T s = (T)0;
   if constexpr (MODEL == IPMC_MODEL_LORENZ63) {
     T g[6];
-    l63_forward<T, FM>(th0[0] + v[0], th0[1] + v[vstride], th0[2] + v[2 * vstride], (const T*)m.x0, (T)m.dt,
-                       m.n_steps, g);
+    l63_G<T, FM>(th0[0] + v[0], th0[1] + v[vstride], th0[2] + v[2 * vstride], (const T*)m.x0, (T)m.dt, m.n_steps,
+                 g);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const T r = (y[i] - g[i]) * ginv[i];
@@ -540,7 +611,7 @@ __global__ __launch_bounds__(kSmallBlock) void small_eval_kernel(const ipmc_mode
     const T* th0 = (const T*)m.theta0;
     if constexpr (MODEL == IPMC_MODEL_LORENZ63) {
       T g[6];
-      l63_forward<T, FM>(th0[0] + v[0], th0[1] + v[1], th0[2] + v[2], (const T*)m.x0, (T)m.dt, m.n_steps, g);
+      l63_G<T, FM>(th0[0] + v[0], th0[1] + v[1], th0[2] + v[2], (const T*)m.x0, (T)m.dt, m.n_steps, g);
 #pragma unroll
       for (int i = 0; i < 6; ++i) out[chain * 6 + i] = g[i];
     } else {

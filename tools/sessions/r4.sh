@@ -46,5 +46,33 @@ case "$1" in
     timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc32/sq -o run -- $B --dtype f32 > /dev/null &&
     python tools/pmc_summarize.py $O/pmc32 f32 65536 $O/pmc_l96_f32.json 6
     ;;
+  s12)
+    # everything the first box can give: the misfit-noise probe and a first
+    # stationary arith comparison, the whole GPU suite (no -x: one statistical
+    # failure must not hide the rest), the line with its same-box profiles,
+    # then the config-5-shape precision comparison
+    timeout -k 10 120 python tools/posterior_agreement.py chaos > $O/chaos.jsonl &&
+    timeout -k 10 300 python tools/posterior_agreement.py arith 8192 48 50 0.2 >> $O/explore.jsonl &&
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; } &&
+    bash tools/sessions/r4.sh s2prof &&
+    timeout -k 10 420 python tools/posterior_agreement.py prec 16384 24 50 0.2 >> $O/explore.jsonl
+    ;;
+  s2prof)
+    B="python bench.py --kernel-only --no-cpu --steps 5 --warmup 1"
+    SQC="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc64/fetch -o run -- $B > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc64/write -o run -- $B > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc64/sq -o run -- $B > /dev/null &&
+    python tools/pmc_summarize.py $O/pmc64 f64 65536 $O/pmc_l96_f64.json 6 &&
+    timeout -k 10 600 python bench.py --pmc-file $O/pmc_l96_f64.json > $O/bench_line.json 2> $O/bench_line.err &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+        python bench.py --kernel-only --no-cpu > $O/bench_kernel_only.json 2> $O/bench_kernel_only.err &&
+    python tools/trace_summary.py $O/trace 200 10 $O/bench_line.json > $O/bench_kernel_trace_summary.json &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc32/fetch -o run -- $B --dtype f32 > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc32/write -o run -- $B --dtype f32 > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc32/sq -o run -- $B --dtype f32 > /dev/null &&
+    python tools/pmc_summarize.py $O/pmc32 f32 65536 $O/pmc_l96_f32.json 6
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
