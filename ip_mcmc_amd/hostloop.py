@@ -335,7 +335,11 @@ def run_structured(plan, U, phi, seed, chain_offset, step, prop_i, n_burn, n_sam
                     elif reach:
                         reach = bool(obj(np.array(v)))
                 if reach:
-                    g = np.atleast_1d(np.asarray(misfit.G(np.array(v)), dtype=np.float64)).reshape(-1).tolist()
+                    gv = misfit.G(np.array(v))
+                    if isinstance(gv, (float, np.floating)):  # a scalar observation (config 1's np.dot)
+                        g = [float(gv)]
+                    else:
+                        g = np.atleast_1d(np.asarray(gv, dtype=np.float64)).reshape(-1).tolist()
                     if len(g) != len(yl):
                         raise ValueError(f"the forward map returned {len(g)} values per parameter vector, the data "
                                          f"have {len(yl)}")

@@ -19,6 +19,13 @@ def test_help_lists_the_options():
     r = _bench("--help")
     assert r.returncode == 0 and "--scaling" in r.stdout and "--dist-backend" in r.stdout
     assert "--steps-per-launch" in r.stdout
+    for opt in ("--workload", "--kernel-only", "--pmc-file", "--no-configs"):
+        assert opt in r.stdout, opt
+
+
+def test_unknown_workload_is_refused():
+    r = _bench("--workload", "cfg9")
+    assert r.returncode != 0 and "invalid choice" in r.stderr
 
 
 def test_world_size_must_equal_gpus():

@@ -43,3 +43,20 @@ def test_stuart_examples_reach_the_exact_posterior(dev, example):
     assert np.all(np.abs(r["mean_error_in_mcse"]) < 4), r
     assert np.allclose(r["posterior_var"], r["exact_var"], rtol=0.1), r
     assert 0.05 < r["accept_rate"] < 0.95, r
+
+
+def test_sharded_config5_example_one_gpu(dev):
+    """examples/sharded_config5.py (config 5 through shard.run_sharded) on one
+    GPU with a reduced ensemble: both precisions run and report a finite
+    posterior-mean difference."""
+    import json
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, os.path.join(REPO, "examples", "sharded_config5.py"), "2048", "2"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = [json.loads(line) for line in p.stdout.splitlines() if line.startswith("{")]
+    assert [r.get("dtype") for r in recs[:2]] == ["float64", "float32"]
+    assert all(r["pcn_steps_per_s"] > 0 and r["chains"] == 2048 for r in recs[:2])
+    assert np.isfinite(recs[2]["posterior_mean_max_abs_diff_f32_f64"])
