@@ -18,6 +18,9 @@
  *                        ipmc_normal
  *   ipmc_host_uniform    rng.random() (accepter.py:62); twin of ipmc_uniform
  *   ipmc_host_step_uniforms  further rng.random() calls within one step
+ *   ipmc_host_ordered_sum    the chain-ordered sum behind the posterior mean over
+ *                        many chains (shard.ordered_mean; np.mean over samples
+ *                        in the reference's one-chain scripts)
  *
  * Host pointers only.  Returns IPMC_OK (0) or an IPMC_ERR_* code of ipmc.h;
  * ipmc_host_last_error() gives the message (thread-local).
@@ -56,6 +59,15 @@ int ipmc_host_uniform(uint64_t seed, int64_t chain_offset, int64_t n_chains, uin
  * uniform (slot 0xFFFFFFFF), i > 0 slot 0xFFFFFFFF - i -- the extra uniforms
  * a caller's own accepter may draw in a step (MCMCSampler's generic host tier). */
 int ipmc_host_step_uniforms(uint64_t seed, int64_t chain, uint64_t step, int32_t n, double* out);
+
+/* acc[j] = (((acc[j] + rows[0][j]/div) + rows[1][j]/div) + ...) over the n_rows
+ * rows (row r at rows + r*row_stride, f64) strictly in row order: the chain-
+ * ordered posterior-mean sum of shard.ordered_mean / run_sharded, the same
+ * bits for any split of the rows over ranks (each continues the previous
+ * rank's acc).  Replaces the reference's np.mean over its one chain's samples
+ * (the reduction a many-chain run adds). */
+int ipmc_host_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div,
+                          double* acc);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,7 @@ SIGNATURES = {
     "ipmc_host_normal": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, C.c_int32, C.c_int32, _P]),
     "ipmc_host_uniform": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, C.c_uint64, _P]),
     "ipmc_host_step_uniforms": (C.c_int, [C.c_uint64, C.c_int64, C.c_uint64, C.c_int32, _P]),
+    "ipmc_host_ordered_sum": (C.c_int, [_P, C.c_int64, C.c_int64, C.c_int64, C.c_double, _P]),
 }
 
 _lib = None
@@ -95,3 +96,14 @@ def extra_uniforms(seed, chain, step, n):
     out = np.empty(n, dtype=np.float64)
     call("ipmc_host_step_uniforms", seed, chain, step, n, _ptr(out))
     return out
+
+
+def ordered_sum(rows, acc, div=1.0):
+    """acc (k,) + rows[0]/div + rows[1]/div + ... strictly in row order, in place
+    (rows: (n, k) float64, C-contiguous rows)."""
+    a = np.ascontiguousarray(rows, dtype=np.float64).reshape(len(rows), -1) if len(rows) else None
+    if a is None:
+        return acc
+    assert acc.dtype == np.float64 and acc.flags.c_contiguous and acc.shape[0] == a.shape[1]
+    call("ipmc_host_ordered_sum", _ptr(a), a.shape[0], a.shape[1], a.shape[1], float(div), _ptr(acc))
+    return acc

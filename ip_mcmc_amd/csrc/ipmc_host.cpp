@@ -143,4 +143,18 @@ int ipmc_host_step_uniforms(uint64_t seed, int64_t chain, uint64_t step, int32_t
   return IPMC_OK;
 }
 
+int ipmc_host_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div,
+                          double* acc) {
+  if (n_rows < 0 || k < 0 || row_stride < k) return fail(IPMC_ERR_INVALID, "bad shape");
+  if (n_rows == 0 || k == 0) return IPMC_OK;
+  if (!rows || !acc) return fail(IPMC_ERR_INVALID, "NULL pointer");
+  // row by row, every column in its own sequential chain (the compiler may
+  // vectorise across columns: each column's additions keep their order)
+  for (int64_t r = 0; r < n_rows; ++r) {
+    const double* x = rows + r * row_stride;
+    for (int64_t j = 0; j < k; ++j) acc[j] = acc[j] + x[j] / div;
+  }
+  return IPMC_OK;
+}
+
 }  // extern "C"

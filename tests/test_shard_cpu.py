@@ -99,23 +99,28 @@ def test_sharded_run_equals_single_process(tmp_path, world):
 
 
 def test_ordered_mean_equals_the_sequential_loop():
-    """The blocked cumsum is the same sequential sum as a row-by-row loop, bit
-    for bit, at 10^5 rows (block boundaries inside), incl. mixed magnitudes."""
+    """ipmc_host_ordered_sum is the same sequential sum as a row-by-row loop,
+    bit for bit, at 10^5 rows incl. mixed magnitudes; with div it equals the
+    loop over row/div (run_sharded's per-chain time averages)."""
     import numpy as np
     import torch
 
-    from ip_mcmc_amd.shard import ordered_mean
+    from ip_mcmc_amd.shard import _seq_sum, ordered_mean
 
     rng = np.random.default_rng(0)
     a = rng.normal(size=(100_000, 7)) * np.exp(rng.normal(scale=8, size=(100_000, 1)))
     acc = np.zeros(7)
     for row in a:
         acc = acc + row
-    want = acc / a.shape[0]
-    assert np.array_equal(ordered_mean(torch.from_numpy(a)), want)
-    assert np.array_equal(ordered_mean(torch.from_numpy(a), block=4096), want)
-    assert np.array_equal(ordered_mean(a[:1000], block=7), ordered_mean(torch.from_numpy(a[:1000])))
-    assert np.array_equal(ordered_mean(a[:5], block=3), np.cumsum(a[:5], axis=0)[-1] / 5)
+    assert np.array_equal(ordered_mean(torch.from_numpy(a)), acc / a.shape[0])
+    assert np.array_equal(ordered_mean(a[:5]), np.cumsum(a[:5], axis=0)[-1] / 5)
+    acc = np.zeros(7)
+    for row in a[:3000]:
+        acc = acc + row / 37.0
+    assert np.array_equal(ordered_mean(a[:3000], div=37.0), acc / 3000)
+    # a split at any row continues the same sum (the rank-sequential scheme)
+    part = _seq_sum(a[:1234], np.zeros(7))
+    assert np.array_equal(_seq_sum(a[1234:], part), _seq_sum(a, np.zeros(7)))
 
 
 # ---------------------------------------------- shard.run_sharded (product)
