@@ -1,7 +1,7 @@
 """Stationary posterior comparisons behind the stated floating-point tolerances.
 
-  python tools/posterior_agreement.py arith  [chains] [segments] [seg_len] [beta] [r]
-  python tools/posterior_agreement.py prec   [chains] [segments] [seg_len] [beta] [r]
+  python tools/posterior_agreement.py arith  [chains] [segments] [seg_len] [beta] [r] [nopair]
+  python tools/posterior_agreement.py prec   [chains] [segments] [seg_len] [beta] [r] [nopair]
   -> one JSON line per comparison
 
 Two pairs of samplers are compared on the same posterior:
@@ -257,4 +257,5 @@ if __name__ == "__main__":
     seg_len = int(a[2]) if len(a) > 2 else 50
     beta = float(a[3]) if len(a) > 3 else 0.2
     r = float(a[4]) if len(a) > 4 else R_NOISE
-    print(json.dumps(measure(kind, chains, n_seg, seg_len, beta, r)), flush=True)
+    paired = not (len(a) > 5 and a[5] == "nopair")
+    print(json.dumps(measure(kind, chains, n_seg, seg_len, beta, r, paired=paired)), flush=True)

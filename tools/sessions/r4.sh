@@ -74,5 +74,22 @@ case "$1" in
     timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc32/sq -o run -- $B --dtype f32 > /dev/null &&
     python tools/pmc_summarize.py $O/pmc32 f32 65536 $O/pmc_l96_f32.json 6
     ;;
+  s3)
+    # stationary-posterior calibration (noise level r, beta, run length) and
+    # the Lorenz-63 fp32 packing A/B on config 2 (interleaved with the product)
+    P="python tools/posterior_agreement.py"
+    V=ip_mcmc_amd/lib/variants/l63scalar/libipmc.so
+    for cfg in "1.0 0.2" "2.0 0.2" "1.0 0.5" "2.0 0.5"; do
+      set -- $cfg
+      timeout -k 10 200 $P arith 8192 48 50 $2 $1 nopair >> $O/calib_arith.jsonl || exit 1
+    done &&
+    timeout -k 10 300 $P arith 8192 96 50 0.3 1.0 nopair >> $O/calib_arith.jsonl &&
+    timeout -k 10 300 $P prec 4096 24 50 0.3 2.0 nopair >> $O/calib_prec.jsonl &&
+    timeout -k 10 300 $P prec 4096 24 50 0.3 4.0 nopair >> $O/calib_prec.jsonl &&
+    timeout -k 10 200 python tools/config_bench.py cfg2 >> $O/l63_pk_ab.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 200 python tools/config_bench.py cfg2 >> $O/l63_pk_ab.jsonl &&
+    timeout -k 10 200 python tools/config_bench.py cfg2 >> $O/l63_pk_ab.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 200 python tools/config_bench.py cfg2 >> $O/l63_pk_ab.jsonl
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
