@@ -5,7 +5,10 @@ bench.py times the FMA forward map; the chains pinned bit for bit to the
 reference fixtures run REFERENCE arith (no FMA, lorenz.py:77-81's order).
 tools/posterior_agreement.py (`arith`) runs both on the forcing-field
 posterior at the headline shape (Lorenz-96 d=40, 2 000 RK4 steps, f64) with
-the reference's own noise recipe (lorenz_mcmc.py:100-112, r = 0.5), from
+the reference's own noise recipe (lorenz_mcmc.py:100-112: γ = r·sd(X_k)) at
+r = 2, where the chaotic time average's misfit noise is below one unit
+(sqrt(d)·σ_ε/γ ≈ 0.5; at the reference's r = 0.5 it is ~2 and the chains
+stick: R̂ 2.1 after 2 400 steps, profiles/r4/posterior_explore_r05.jsonl), from
 independent prior draws u_0 with independent Philox seeds, long enough to
 reach stationarity; it discards the burn-in diagnostics.burn_in_lengths finds
 and estimates Monte-Carlo standard errors by batch means.  The stated
@@ -35,8 +38,8 @@ PAIRED_MIN = 0.99
 Z_MAX = 4.0
 BAND = 3.5 * np.sqrt(2 / D)
 RHAT_MAX = 1.1
-# (chains, blocks, steps per block, beta): 2 400 pCN steps per chain
-RUN = (8192, 48, 50, 0.2)
+# (chains, blocks, steps per block, beta, noise level r): 4 800 pCN steps per chain
+RUN = (8192, 96, 50, 0.3, 2.0)
 
 
 def test_fma_and_reference_posteriors_agree_at_the_headline_shape():
@@ -45,8 +48,8 @@ def test_fma_and_reference_posteriors_agree_at_the_headline_shape():
     import posterior_agreement as PA
 
     assert torch.cuda.is_available()
-    chains, n_seg, seg_len, beta = RUN
-    r = PA.measure("arith", chains, n_seg, seg_len, beta)
+    chains, n_seg, seg_len, beta, noise_r = RUN
+    r = PA.measure("arith", chains, n_seg, seg_len, beta, noise_r)
     print(r)
     assert r["d"] == D and r["rk4_steps"] == 2000 and r["chains"] == chains
     assert "burn_in_capped_from" not in r, r  # the burn-in ends inside the run

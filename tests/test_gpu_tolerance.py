@@ -4,7 +4,8 @@ floating-point tolerance.
 Per chain the two precisions part ways under the chaotic forward map, so the
 bar is statistical.  tools/posterior_agreement.py (`prec`) runs fp64 and fp32
 on the forcing-field posterior at d=256 with config 5's 10 000 RK4 steps per
-forward map (the reference's noise recipe, lorenz_mcmc.py:100-112, r = 0.5),
+forward map (the reference's noise recipe, lorenz_mcmc.py:100-112, γ = r·sd(X_k)
+at r = 2: misfit noise below one unit; at r = 0.5, R̂ 2.7 after 1 200 steps),
 from independent prior draws u_0 with independent Philox seeds, discards the
 burn-in diagnostics.burn_in_lengths finds and estimates Monte-Carlo standard
 errors by batch means.  The stated tolerance:
@@ -31,8 +32,8 @@ D = 256
 Z_MAX = 4.5
 BAND = 3.5 * np.sqrt(2 / D)
 RHAT_MAX = 1.1
-# (chains, blocks, steps per block, beta)
-RUN = (16384, 24, 50, 0.2)
+# (chains, blocks, steps per block, beta, noise level r): 2 400 pCN steps per chain
+RUN = (8192, 48, 50, 0.3, 2.0)
 
 
 def test_fp32_and_fp64_posteriors_agree_at_config5_shape():
@@ -41,8 +42,8 @@ def test_fp32_and_fp64_posteriors_agree_at_config5_shape():
     import posterior_agreement as PA
 
     assert torch.cuda.is_available()
-    chains, n_seg, seg_len, beta = RUN
-    r = PA.measure("prec", chains, n_seg, seg_len, beta)
+    chains, n_seg, seg_len, beta, noise_r = RUN
+    r = PA.measure("prec", chains, n_seg, seg_len, beta, noise_r)
     print(r)
     assert r["d"] == D and r["rk4_steps"] == 10000 and r["chains"] == chains
     assert "burn_in_capped_from" not in r, r

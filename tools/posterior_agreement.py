@@ -14,14 +14,14 @@ Two pairs of samplers are compared on the same posterior:
 The posterior.  The forcing-field problem of bench.py (F = 8 + u, u_true =
 0.5 sin(2πk/d), prior N(0, I), y = G(u_true) + η) with the reference's own
 noise recipe (lorenz_mcmc.py:100-112: Γ = r²·diag(var of the observed
-quantity along the truth's trajectory), r = 0.5): γ = r·sd(X_k).  bench.py's
-γ = 0.1 is a throughput workload, not a posterior any chain reaches in a
-feasible run: the time-averaged observation of a chaotic run fluctuates by
-σ_ε ≈ 0.5 (d=40, T=10) / 0.3 (d=256, T=50) under any proposal a pCN step can
-make (tools/posterior_agreement.py chaos), so with γ = 0.1 every proposal
-re-draws ~½Σ(ε/γ)² ≈ 500 units of misfit and the chains freeze where they land
-(0.2 % accepted, falling).  With γ = r·sd(X) ≈ 1.8 the misfit noise is O(1)
-and the chains mix.
+quantity along the truth's trajectory)): γ = r·sd(X_k).  The time-averaged
+observation of a chaotic run moves by σ_ε ≈ 0.5 (d=40, T=10) / 0.3 (d=256,
+T=50) under any perturbation a pCN step makes (`chaos`), so each proposal's
+misfit carries a noise of sd ≈ sqrt(d)·σ_ε/γ: with bench.py's γ = 0.1 that is
+~50 units (the chains freeze where they land: 0.2 % accepted, falling), at the
+reference's r = 0.5 (γ ≈ 1.8) ~2 (8-9 % accepted, the chains stick: split-R̂
+2.1 after 2 400 steps at d=40, profiles/r4/posterior_explore_r05.jsonl), at
+r = 2 (γ ≈ 7.3) ~0.5: a noisy-likelihood chain that mixes.
 
 The run.  Independent u_0 for each sampler, drawn from the prior (over-
 dispersed against the posterior) with independent seeds, and independent
@@ -63,7 +63,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 DT = 0.005
-R_NOISE = 0.5  # lorenz_mcmc.py:111-112's noise level r
+R_NOISE = 2.0  # the noise level r of lorenz_mcmc.py:111-112 (the reference used 0.5 for its 5K moments)
 
 
 def truth_sd(d, F, n_spin=2000, n_traj=20000, dt=DT):
