@@ -289,7 +289,8 @@ def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="a
            "steps": steps, "total_chains": total_chains, "chains_per_gpu": total_chains // world,
            "accept_rate": float(res["accepts"].sum()) / (total_chains * steps),
            "run_seconds_rank0": res["run_seconds"], "gather_ms": res["gather_seconds"] * 1e3,
-           "setup_ms": tm["setup_s"] * 1e3, "sweeps_gpu_ms": tm["sweeps_gpu_ms"], "tail_ms": tm["tail_ms"]}
+           "setup_ms": tm["setup_s"] * 1e3, "phi0_gpu_ms": tm["phi0_gpu_ms"], "sweeps_gpu_ms": tm["sweeps_gpu_ms"],
+           "tail_ms": tm["tail_ms"]}
     return rec, res
 
 

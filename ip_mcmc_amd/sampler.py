@@ -260,6 +260,8 @@ class MCMCSampler:
         state_dtype = "float64" if td == torch.float64 else "float32"
         if resume and u_0.phi.shape[0] != n_chains:
             raise ValueError("ChainState phi does not match its u")
+        ev_setup = torch.cuda.Event(enable_timing=True)  # the GPU work of the set-up: Φ(u0)
+        ev_setup.record(torch.cuda.current_stream(device))
         if resume and u_0.dtype == state_dtype and u_0.accept_kind != "generic":
             phi.copy_(dev.to_device(u_0.phi, td, device))
         else:
@@ -460,12 +462,15 @@ class MCMCSampler:
         self.state.steps_this_run = total
         if keep == "samples" and sink is None and not overlap:
             host_out.copy_(samples if samples.dtype == torch.float64 else samples.double())
-        # where the wall time went: set-up (H2D, Φ(u0), plan) before the first
-        # launch, the GPU time of all sweeps, and the rest after set-up that the
-        # sweeps do not cover (launch gaps, the copy tail, host epilogue)
+        # where the wall time went: host set-up (H2D, plan; Φ(u0) is queued) before
+        # the first launch, the GPU time of Φ(u0) and of all sweeps, and the rest
+        # after set-up that the sweeps do not cover (Φ(u0) still running when the
+        # host finished its set-up, launch gaps, the copy tail, host epilogue)
         t_end = time.perf_counter()
         sweeps_ms = ev_first.elapsed_time(ev_swept)
-        self.last_run_timing = {"total_s": t_end - t_entry, "setup_s": t0 - t_entry, "sweeps_gpu_ms": sweeps_ms,
+        phi0_ms = ev_setup.elapsed_time(ev_first)
+        self.last_run_timing = {"total_s": t_end - t_entry, "setup_s": t0 - t_entry, "phi0_gpu_ms": phi0_ms,
+                                "sweeps_gpu_ms": sweeps_ms,
                                 "tail_ms": (t_end - t0) * 1e3 - sweeps_ms, "copy_overlapped": bool(overlap)}
         if keep == "samples":
             if sink is not None:
