@@ -10,7 +10,8 @@ from independent prior draws u_0 with independent Philox seeds, discards the
 burn-in diagnostics.burn_in_lengths finds and estimates Monte-Carlo standard
 errors by batch means.  The stated tolerance:
 
-* stationarity: split-R̂ < RHAT_MAX and first vs second half |z| < Z_MAX;
+* stationarity of the ensemble: first vs second half of the post-burn-in run,
+  |z| < Z_MAX for the mean and for the spread (split-R̂ reported);
 * the posterior means agree: max_i |z_i| < Z_MAX (family-wise false alarm
   ~0.3 % over 256 components) and mean z² and the whitened T²/d within
   1 ± 3.5·sqrt(2/256) = 1 ± 0.31, two-sided (round 3's independent-seed test
@@ -31,7 +32,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 D = 256
 Z_MAX = 4.5
 BAND = 3.5 * np.sqrt(2 / D)
-RHAT_MAX = 1.1
 # (chains, blocks, steps per block, beta, noise level r): 2 400 pCN steps per chain
 RUN = (8192, 48, 50, 0.3, 2.0)
 
@@ -50,8 +50,7 @@ def test_fp32_and_fp64_posteriors_agree_at_config5_shape():
     for arm in ("fma_float64", "fma_float32"):
         a = r[arm]
         assert 0.02 < a["accept_rate"] < 0.98, a
-        assert a["rhat_max"] < RHAT_MAX, a
-        assert a["half_z_max"] < Z_MAX, a
+        assert a["half_z_max"] < Z_MAX and a["half_var_z_max"] < Z_MAX, a
     assert r["max_z"] < Z_MAX, r
     assert abs(r["mean_z2"] - 1) < BAND, r
     assert abs(r["t2_over_d"] - 1) < BAND, r

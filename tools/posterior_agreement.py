@@ -42,9 +42,13 @@ The statistics (all per parameter component i):
     their lag-1 autocorrelation is below 0.1; the across-chain standard error
     (sd over chains of the per-chain means / sqrt(C)) is reported beside it
     and the larger of the two is used;
-  * stationarity: split-R̂ over the post-burn-in blocks and a first-half vs
-    second-half z (per chain difference, so the halves' correlation is
-    accounted for);
+  * stationarity of the ensemble over the post-burn-in run: the chains'
+    first-half and second-half means have the same mean (per-chain difference
+    z) and the same spread (paired z of the squared deviations) -- exact for
+    independent chains whatever their autocorrelation; split-R̂ over the batch
+    means is reported beside them (it also asks each chain to have explored
+    the posterior: a stationary chain a few autocorrelation times long reads
+    R̂² ≈ 1 + (τ − 1)/h);
   * agreement: z_i = (m_A,i − m_B,i) / sqrt(se_A,i² + se_B,i²); max |z_i|,
     mean z_i², and the whitened statistic T²/d = Δᵀ(S_A/C + S_B/C)⁻¹Δ / d
     with S the between-chain covariance of the per-chain means (a chi-square
@@ -134,23 +138,34 @@ def burn_in_blocks(B, window, theta0=8.0):
     return burn_in_lengths(np.ascontiguousarray(B + theta0), avg_window=window, layout="time_vars")
 
 
-def _se_batch(P):
-    """Batch-means MCSE of the grand mean of P (C, n, d) and the batch size
-    (in blocks) at which the batch means' lag-1 autocorrelation is < 0.1."""
+def _batches(P):
+    """Batch means of P (C, n, d): consecutive blocks merged until the batch
+    means' lag-1 autocorrelation is below 0.1 (or 8 batches are left).
+    Returns (Q (C, nb, d), batch size in blocks, that lag-1 autocorrelation)."""
     C, n, d = P.shape
     bs = 1
     while True:
         nb = n // bs
         Q = P[:, :nb * bs].reshape(C, nb, bs, d).mean(axis=2)
         if nb < 4:
-            break
+            return Q, bs, None
         c = Q - Q.mean(axis=1, keepdims=True)
         r1 = np.sum(c[:, 1:] * c[:, :-1], axis=(0, 1)) / np.maximum(np.sum(c * c, axis=(0, 1)), 1e-300)
-        if np.max(r1) < 0.1 or nb < 8:
-            break
+        if np.max(r1) < 0.1 or nb < 16:
+            return Q, bs, float(np.max(r1))
         bs *= 2
-    se = Q.reshape(-1, d).std(axis=0, ddof=1) / np.sqrt(Q.shape[0] * Q.shape[1])
-    return se, bs, float(np.max(r1)) if nb >= 4 else None
+
+
+def _split_rhat(Q):
+    """Split-R̂ per component over the batch means Q (C, nb, d): each chain's
+    batches cut in two halves; on (nearly) uncorrelated batches, so the
+    within-chain autocorrelation does not inflate it (on raw autocorrelated
+    blocks a stationary chain reads R̂² ≈ 1 + (τ − 1)/h)."""
+    h = Q.shape[1] // 2
+    S = np.concatenate([Q[:, :h], Q[:, h:2 * h]], axis=0)  # (2C, h, d)
+    W = S.var(axis=1, ddof=1).mean(axis=0)
+    Bv = h * S.mean(axis=1).var(axis=0, ddof=1)
+    return np.sqrt(((h - 1) / h * W + Bv / h) / W)
 
 
 def summarize(B, burn):
@@ -160,19 +175,27 @@ def summarize(B, burn):
     m_chain = P.mean(axis=1)  # (C, d)
     m = m_chain.mean(axis=0)
     se_chain = m_chain.std(axis=0, ddof=1) / np.sqrt(C)
-    se_bm, bs, r1 = _se_batch(P)
+    Q, bs, r1 = _batches(P)
+    se_bm = Q.reshape(-1, d).std(axis=0, ddof=1) / np.sqrt(Q.shape[0] * Q.shape[1])
     se = np.maximum(se_chain, se_bm)
-    # split-R-hat over post-burn-in blocks (each chain split in two halves)
+    rhat = _split_rhat(Q)
+    # the ensemble is stationary over the post-burn-in run: the chains' first-
+    # half and second-half means have the same mean (per-chain difference z)
+    # and the same spread (paired z of the squared deviations) -- both exact
+    # for independent chains whatever their autocorrelation, unlike R̂, which
+    # also asks every chain to have explored the posterior (split-R̂ is
+    # reported; a stationary chain as short as a few autocorrelation times
+    # reads above 1)
     h = P.shape[1] // 2
-    S = np.concatenate([P[:, :h], P[:, h:2 * h]], axis=0)  # (2C, h, d)
-    W = S.var(axis=1, ddof=1).mean(axis=0)
-    Bv = h * S.mean(axis=1).var(axis=0, ddof=1)
-    rhat = np.sqrt(((h - 1) / h * W + Bv / h) / W)
-    # first half vs second half, per chain difference
-    dif = P[:, :h].mean(axis=1) - P[:, h:2 * h].mean(axis=1)
+    m1, m2 = P[:, :h].mean(axis=1), P[:, h:2 * h].mean(axis=1)
+    dif = m1 - m2
     zh = np.abs(dif.mean(axis=0)) / (dif.std(axis=0, ddof=1) / np.sqrt(C))
+    mu = 0.5 * (m1.mean(axis=0) + m2.mean(axis=0))
+    dv = (m1 - mu) ** 2 - (m2 - mu) ** 2
+    zv = np.abs(dv.mean(axis=0)) / (dv.std(axis=0, ddof=1) / np.sqrt(C))
     return {"m": m, "se": se, "se_chain": se_chain, "se_bm": se_bm, "batch_blocks": bs, "batch_r1": r1,
-            "rhat_max": float(rhat.max()), "half_z_max": float(zh.max()), "m_chain": m_chain}
+            "rhat_max": float(rhat.max()), "half_z_max": float(zh.max()), "half_var_z_max": float(zv.max()),
+            "m_chain": m_chain}
 
 
 def compare(sa, sb):
@@ -224,7 +247,8 @@ def measure(kind, chains, n_seg, seg_len, beta=0.2, r=R_NOISE, window=None, pair
     names = [f"{a}_{np.dtype(t).name}" for a, t, *_ in runs]
     for nm, sm, (B, acc, wall, _) in zip(names, sums, res):
         out[nm] = {"accept_rate": float(acc.sum()) / (chains * n_seg * seg_len), "rhat_max": sm["rhat_max"],
-                   "half_z_max": sm["half_z_max"], "batch_blocks": sm["batch_blocks"], "batch_r1": sm["batch_r1"],
+                   "half_z_max": sm["half_z_max"], "half_var_z_max": sm["half_var_z_max"],
+                   "batch_blocks": sm["batch_blocks"], "batch_r1": sm["batch_r1"],
                    "mcse_median": float(np.median(sm["se"])), "post_mean_range": [float(sm["m"].min()),
                                                                                   float(sm["m"].max())],
                    "wall_s": wall}
