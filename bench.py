@@ -331,7 +331,7 @@ def config_line(key, dev, world, steps=None, warmup=None, chains=None):
     prob = make_problem(key)
     total = chains or prob.chains
     st, wu = steps or prob.steps, prob.warmup if warmup is None else warmup
-    gather = "mean" if key == "cfg5" else "all"
+    gather = "mean"
     rec64, r64 = timed_run(prob, np.float64, dev, total, st, wu, world, gather=gather)
     out = {"workload": prob.name, "f64": rec64, "flop_per_chain_step": prob.flop,
            "tflops_f64": total * prob.flop * st / rec64["wall_s"] / 1e12}
@@ -489,7 +489,10 @@ def main():
         args.no_extra = args.no_configs = args.no_cpu = True
 
     # 2. value: MCMCSampler.run end to end through shard.run_sharded
-    gather_mode = "mean" if total_chains * prob.k > (1 << 26) else "all"
+    # the job's result on every rank: the posterior mean (rank-sequential
+    # ordered sum, bit-identical for any N) and every chain's Φ and accept
+    # count; the per-chain states and sums stay on their rank
+    gather_mode = "mean"
     if args.kernel_only:
         e2e = {"pcn_steps_per_s": kernel_rate, "wall_s": el_k, "ms_per_step": el_k / steps * 1e3,
                "accept_rate": None, "gather_ms": 0.0, "kernel_only": True}
@@ -501,6 +504,8 @@ def main():
     log(f"end-to-end: {e2e['wall_s']:.3f} s, {value / 1e6:.2f} M steps/s")
     gather = {"ms": e2e["gather_ms"], "mode": gather_mode,
               "bytes_per_rank": int(per_rank * (3 * prob.k + 2) * 8 if gather_mode == "all" else per_rank * 16),
+              "what": "every chain's Phi and accept count (all_gather_into_tensor) and the posterior mean "
+                      "(rank-sequential ordered sum of the per-chain time averages, send/recv of k doubles per rank)",
               "collective": (f"all_gather_into_tensor ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
                              + (" + rank-sequential ordered sum (send/recv)" if gather_mode == "mean" else "")
                              if world > 1 else "none (one rank)"),

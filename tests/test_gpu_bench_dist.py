@@ -40,6 +40,7 @@ def test_bench_two_ranks_rehearsal():
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["config"]["total_chains"] == 8192
     assert line["final_gather"]["rows"] == 8192 and "gloo" in line["final_gather"]["collective"]
+    assert line["final_gather"]["mode"] == "mean"
     assert line["value"] > 0 and 0 < line["accept_rate"] < 1
 
 
