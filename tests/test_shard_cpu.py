@@ -197,3 +197,35 @@ def test_run_sharded_mean_by_rank_sequential_sum(tmp_path):
     for key in ("mean", "phi", "accepts"):
         assert np.array_equal(got[key], one[key]), key
     assert got["sum_u"].shape[0] == 12  # rank 1's own block of chain_range(37, 1, 3)
+
+
+def _sharded_file_worker(rank, world, port, prefix):
+    import sys
+
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import run_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(C_TOTAL, 4))
+    res = run_sharded(_lin_sampler_factory(), u0, n_samples=6, burn_in=9, sample_interval=4, keep="samples",
+                      sample_file=prefix)
+    assert "samples" not in res and res["u"].shape == (C_TOTAL, 4)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_run_sharded_streams_each_ranks_samples_to_its_own_file(tmp_path):
+    """keep='samples' with sample_file: rank r streams its block of chains to
+    <prefix>.rank<r>.npy; the files concatenated in rank order are the
+    one-process samples."""
+    from ip_mcmc_amd.shard import chain_range
+
+    prefix = str(tmp_path / "chains")
+    mp.start_processes(_sharded_file_worker, args=(3, _free_port(), prefix), nprocs=3, start_method="spawn")
+    parts = [np.load(f"{prefix}.rank{r}.npy") for r in range(3)]
+    assert [p.shape[0] for p in parts] == [b - a for a, b in (chain_range(C_TOTAL, r, 3) for r in range(3))]
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(C_TOTAL, 4))
+    one = _lin_sampler_factory()(0).run(u0, n_samples=6, burn_in=9, sample_interval=4)
+    np.testing.assert_array_equal(np.concatenate(parts, axis=0), one)
