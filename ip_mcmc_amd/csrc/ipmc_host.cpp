@@ -148,11 +148,23 @@ int ipmc_host_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t
   if (n_rows < 0 || k < 0 || row_stride < k) return fail(IPMC_ERR_INVALID, "bad shape");
   if (n_rows == 0 || k == 0) return IPMC_OK;
   if (!rows || !acc) return fail(IPMC_ERR_INVALID, "NULL pointer");
-  // row by row, every column in its own sequential chain (the compiler may
-  // vectorise across columns: each column's additions keep their order)
-  for (int64_t r = 0; r < n_rows; ++r) {
-    const double* x = rows + r * row_stride;
-    for (int64_t j = 0; j < k; ++j) acc[j] = acc[j] + x[j] / div;
+  // row by row, every column in its own sequential chain, in column tiles
+  // held in registers (the columns vectorise: each one's additions keep
+  // their order); div == 1 adds the rows as they are
+  constexpr int64_t kTile = 64;
+  for (int64_t j0 = 0; j0 < k; j0 += kTile) {
+    const int64_t nj = k - j0 < kTile ? k - j0 : kTile;
+    double a[kTile];
+    for (int64_t j = 0; j < nj; ++j) a[j] = acc[j0 + j];
+    const double* __restrict__ x = rows + j0;
+    if (div == 1.0) {
+      for (int64_t r = 0; r < n_rows; ++r, x += row_stride)
+        for (int64_t j = 0; j < nj; ++j) a[j] = a[j] + x[j];
+    } else {
+      for (int64_t r = 0; r < n_rows; ++r, x += row_stride)
+        for (int64_t j = 0; j < nj; ++j) a[j] = a[j] + x[j] / div;
+    }
+    for (int64_t j = 0; j < nj; ++j) acc[j0 + j] = a[j];
   }
   return IPMC_OK;
 }

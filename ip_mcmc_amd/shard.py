@@ -123,9 +123,9 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     Returns a dict on every rank:
       "u", "phi", "accepts"   the final chain states (C_total, k), Φ, accept counts
       keep="moments": "sum_u", "sum_u2" (C_total, k) and "n", plus "mean"
-                     (the posterior-mean estimate: the per-chain time averages
-                     averaged over chains in fixed global order, ordered_mean --
-                     bit-identical for any number of ranks)
+                     (the posterior-mean estimate: the per-chain sums added
+                     over the chains in fixed global order, ordered_mean, over
+                     n x C_total -- bit-identical for any number of ranks)
       keep="samples": "samples" (C_total, n_samples, k); with sample_file each
                      rank streams its own block to f"{sample_file}.rank{r}.npy"
                      and nothing is gathered but the state
@@ -173,7 +173,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
             small = gather_chains(torch.from_numpy(np.ascontiguousarray(small)).to(_comm_device(group)), n_total,
                                   group).cpu().numpy()
         n = max(1, res["n"])
-        mean = ordered_sum_sharded(res["sum_u"].reshape(hi - lo, k), group, div=n) / n_total
+        mean = ordered_sum_sharded(res["sum_u"].reshape(hi - lo, k), group) / (float(n) * n_total)
         return {"u": cols[0], "phi": small[:, 0], "accepts": small[:, 1].astype(np.int64), "sum_u": res["sum_u"],
                 "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
                 "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
@@ -208,6 +208,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         elif keep == "last":
             out["last"] = rest
     if keep == "moments":
-        out["mean"] = ordered_mean(out["sum_u"], div=max(1, res["n"]))
+        # Σ over chains (in global order) of the per-chain sums, / (steps × chains) once
+        out["mean"] = ordered_mean(out["sum_u"]) / float(max(1, res["n"]))
     out["gather_seconds"] = time.perf_counter() - t1
     return out
