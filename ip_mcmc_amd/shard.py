@@ -209,6 +209,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
             out["last"] = rest
     if keep == "moments":
         # Σ over chains (in global order) of the per-chain sums, / (steps × chains) once
-        out["mean"] = ordered_mean(out["sum_u"]) / float(max(1, res["n"]))
+        S = _seq_sum(np.asarray(out["sum_u"]), np.zeros(k))
+        out["mean"] = S / (float(max(1, res["n"])) * n_total)
     out["gather_seconds"] = time.perf_counter() - t1
     return out
