@@ -91,6 +91,7 @@ case "$1" in
     timeout -k 10 200 python tools/config_bench.py cfg2 >> $O/l63_pk_ab.jsonl &&
     IPMC_LIB_PATH=$V timeout -k 10 200 python tools/config_bench.py cfg2 >> $O/l63_pk_ab.jsonl &&
     timeout -k 10 200 python tools/config_bench.py ts36 ts36:36 ts36 ts36:36 >> $O/ts36_layouts.jsonl &&
+    timeout -k 10 200 python tools/config_bench.py l96mx1@256 l96mx64@256 l96mx1024@256 l96x1@256 l96x64@256 >> $O/spec_mixing.jsonl &&
     timeout -k 10 600 python -u -m pytest -v --timeout 500 --timeout-method thread \
         tests/test_gpu_arith_agreement.py tests/test_gpu_tolerance.py > $O/pytest_stationary.log 2>&1
     ;;
