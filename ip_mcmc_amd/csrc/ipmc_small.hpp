@@ -271,6 +271,9 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
 #define IPMC_SPEC_BLOCK 256
 #endif
 constexpr int kSpecBlock = IPMC_SPEC_BLOCK;
+#ifndef IPMC_SPEC_K3  // 0: Lorenz-63 with the generic k <= 8 registers (A/B)
+#define IPMC_SPEC_K3 1
+#endif
 constexpr int kSpecKMax = 8;
 // linear G: A [q, k], y [q] and 1/γ [q] staged in LDS when q (k + 2) fits
 constexpr int kSpecLinLds = 1024;
@@ -330,7 +333,11 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   const int gbase = lane & ~(S - 1);
   const unsigned long long gmask = (S == 64) ? ~0ull : ((1ull << S) - 1);
   const int64_t chain = ((int64_t)blockIdx.x * kSpecBlock + t) / S;
-  const int k = m.k;
+  // Lorenz-63 has k = 3 (ipmc_validate_model): the per-chain registers and
+  // the per-round loops are sized to it at compile time
+  constexpr bool K3 = IPMC_SPEC_K3 && MODEL == IPMC_MODEL_LORENZ63;
+  constexpr int KM = K3 ? 3 : kSpecKMax;
+  const int k = K3 ? 3 : m.k;
   // per-problem constants, read once per launch instead of once per round
   bool staged = false;
   if constexpr (MODEL == IPMC_MODEL_LINEAR) {
@@ -359,9 +366,9 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   T* v = vpark + t;                       // this lane's proposal, v[j * kSpecBlock]
   const T* vgroup = vpark + (t - sub);    // lane 0 of the group
   const T* rs = (const T*)s.reg_scale;
-  T ur[kSpecKMax], sqr[kSpecKMax], lor[kSpecKMax], hir[kSpecKMax], offr[kSpecKMax], rsr[kSpecKMax], th0r[kSpecKMax];
+  T ur[KM], sqr[KM], lor[KM], hir[KM], offr[KM], rsr[KM], th0r[KM];
 #pragma unroll
-  for (int j = 0; j < kSpecKMax; ++j) {
+  for (int j = 0; j < KM; ++j) {
     const bool in = j < k;
     ur[j] = in ? u[j] : (T)0;
     sqr[j] = (in && sq) ? sq[j] : (T)0;
@@ -377,23 +384,23 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   int64_t st = 0;
   // PRE: draws of steps [pbase, pbase + C) of this group, in pre_w / pre_lr
   const int grp = (t - sub) / S;  // this group's index in the block
-  T* gw = pre_w + (PRE ? grp * C * kSpecKMax : 0);
+  T* gw = pre_w + (PRE ? grp * C * KM : 0);
   double* glr = pre_lr + (PRE ? grp * C : 0);
   int64_t pbase = 0, pend = 0;
   // w_j of step tt (sqrt(C_jj)·ξ_j or Σ_{i<=j} L_ji ξ_i), in the sequential kernel's order
-  auto draw_w = [&](uint64_t step, T (&w)[kSpecKMax]) {
+  auto draw_w = [&](uint64_t step, T (&w)[KM]) {
     double z0 = 0.0, z1 = 0.0;
-    T xi[kSpecKMax];
+    T xi[(KM + 1) & ~1];
     if (chol) {
 #pragma unroll
-      for (int j = 0; j < kSpecKMax; j += 2) {
+      for (int j = 0; j < KM; j += 2) {
         if (j < k) normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
         xi[j] = (T)z0;
         xi[j + 1] = (T)z1;
       }
     }
 #pragma unroll
-    for (int j = 0; j < kSpecKMax; ++j) {
+    for (int j = 0; j < KM; ++j) {
       w[j] = (T)0;
       if (j < k) {
         if (chol) {
@@ -437,10 +444,10 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
           const int64_t ti = pbase + i;
           if (ti < s.n_steps) {
             const uint64_t step = s.step0 + (uint64_t)ti;
-            T w[kSpecKMax];
+            T w[KM];
             draw_w(step, w);
 #pragma unroll
-            for (int j = 0; j < kSpecKMax; ++j) gw[i * kSpecKMax + j] = w[j];
+            for (int j = 0; j < KM; ++j) gw[i * KM + j] = w[j];
             glr[i] = det_log(accept_uniform(s.seed, gid, step));
           }
         }
@@ -448,24 +455,24 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       }
     }
     // this slot's proposal noise w (step tt)
-    T w[kSpecKMax];
+    T w[KM];
     if (sub < left) {
       if constexpr (PRE) {
         const int pi = (int)(tt - pbase);
 #pragma unroll
-        for (int j = 0; j < kSpecKMax; ++j) w[j] = gw[pi * kSpecKMax + j];
+        for (int j = 0; j < KM; ++j) w[j] = gw[pi * KM + j];
       } else {
         draw_w(s.step0 + (uint64_t)tt, w);
         if (amode) {
 #pragma unroll
-          for (int j = 0; j < kSpecKMax; ++j) wown[j * kSpecBlock] = w[j];
+          for (int j = 0; j < KM; ++j) wown[j * kSpecBlock] = w[j];
         }
       }
     }
     // accept mode: the proposals of the slots before this one, in step order
-    T pv[kSpecKMax];
+    T pv[KM];
 #pragma unroll
-    for (int j = 0; j < kSpecKMax; ++j) pv[j] = ur[j];
+    for (int j = 0; j < KM; ++j) pv[j] = ur[j];
     if (!PRE) wave_sync_lds();  // the parked w of the group's slots
     if (amode) {
       const int64_t lim = left < S ? left : S;
@@ -475,9 +482,9 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
         const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
         const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
 #pragma unroll
-        for (int j = 0; j < kSpecKMax; ++j) {
+        for (int j = 0; j < KM; ++j) {
           if (j < k) {
-            const T wq = PRE ? gw[(int)(tq - pbase) * kSpecKMax + j] : wgroup[j * kSpecBlock + q];
+            const T wq = PRE ? gw[(int)(tq - pbase) * KM + j] : wgroup[j * kSpecBlock + q];
             pv[j] = propose_one<T>(rw, pv[j], wq, cq, bq);
           }
         }
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
       ok = true;
 #pragma unroll
-      for (int j = 0; j < kSpecKMax; ++j) {
+      for (int j = 0; j < KM; ++j) {
         if (j < k) {
           const T vj = propose_one<T>(rw, pv[j], w[j], cs, bs);
           v[j * kSpecBlock] = vj;
@@ -512,7 +519,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
         if (rs) {
           T r2 = (T)0;  // small_regularizer's order
 #pragma unroll
-          for (int j = 0; j < kSpecKMax; ++j) {
+          for (int j = 0; j < KM; ++j) {
             if (j < k) {
               const T tj = rsr[j] * v[j * kSpecBlock];
               r2 = madd<FM>(tj, tj, r2);
@@ -550,11 +557,11 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
     auto last_acc = [&](int q) { return amode ? (q < nar ? q : nar - 1) : (q == first ? first : -1); };
     if (s.sum_u && sub == 0) {
       // the states after each of the `used` steps, in step order
-      RoundSums<kSpecKMax> rsum(s.sum_u + chain * k, s.sum_u2 ? s.sum_u2 + chain * k : nullptr, k);
+      RoundSums<KM> rsum(s.sum_u + chain * k, s.sum_u2 ? s.sum_u2 + chain * k : nullptr, k);
       for (int q = 0; q < used; ++q) {
         const int la = last_acc(q);
 #pragma unroll
-        for (int j = 0; j < kSpecKMax; ++j)
+        for (int j = 0; j < KM; ++j)
           if (j < k) rsum.add(j, la >= 0 ? (double)vgroup[j * kSpecBlock + la] : (double)ur[j]);
       }
       rsum.store();
@@ -566,13 +573,13 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
         const int64_t sl = clk.take(clk.next);
         T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
 #pragma unroll
-        for (int j = 0; j < kSpecKMax; ++j)
+        for (int j = 0; j < KM; ++j)
           if (j < k) so[j] = la >= 0 ? vgroup[j * kSpecBlock + la] : ur[j];
       }
     }
     if (win >= 0) {
 #pragma unroll
-      for (int j = 0; j < kSpecKMax; ++j)
+      for (int j = 0; j < KM; ++j)
         if (j < k) ur[j] = vgroup[j * kSpecBlock + win];
       phu = phf;
     }
@@ -586,12 +593,12 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
     if (s.accepts) s.accepts[chain] += nacc;
     if (s.calls) s.calls[chain] += ncalls;
 #pragma unroll
-    for (int j = 0; j < kSpecKMax; ++j)
+    for (int j = 0; j < KM; ++j)
       if (j < k) u[j] = ur[j];
     if (s.sample_out && s.sample_every == 0) {
       T* so = (T*)s.sample_out + chain * s.sample_stride;
 #pragma unroll
-      for (int j = 0; j < kSpecKMax; ++j)
+      for (int j = 0; j < KM; ++j)
         if (j < k) so[j] = ur[j];
     }
   }

@@ -53,6 +53,7 @@ def test_fma_and_reference_posteriors_agree_at_the_headline_shape():
     chains, n_seg, seg_len, beta, noise_r = RUN
     r = PA.measure("arith", chains, n_seg, seg_len, beta, noise_r)
     print(r)
+    PA.record(r, "posterior_agreement.jsonl")
     assert r["d"] == D and r["rk4_steps"] == 2000 and r["chains"] == chains
     assert "burn_in_capped_from" not in r, r  # the burn-in ends inside the run
     for arm in ("fma_float64", "reference_float64"):

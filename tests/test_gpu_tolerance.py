@@ -45,6 +45,7 @@ def test_fp32_and_fp64_posteriors_agree_at_config5_shape():
     chains, n_seg, seg_len, beta, noise_r = RUN
     r = PA.measure("prec", chains, n_seg, seg_len, beta, noise_r)
     print(r)
+    PA.record(r, "posterior_agreement.jsonl")
     assert r["d"] == D and r["rk4_steps"] == 10000 and r["chains"] == chains
     assert "burn_in_capped_from" not in r, r
     for arm in ("fma_float64", "fma_float32"):

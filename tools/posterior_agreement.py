@@ -216,6 +216,16 @@ def compare(sa, sb):
             "se_ratio_bm_over_chain": float(np.median(sa["se_bm"] / sa["se_chain"]))}
 
 
+def record(rec, name):
+    """Append `rec` to $IPMC_RECORD_DIR/name when the variable is set (GPU
+    sessions keep the tests' measurements beside their log)."""
+    d = os.environ.get("IPMC_RECORD_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
 def measure(kind, chains, n_seg, seg_len, beta=0.2, r=R_NOISE, window=None, paired=True):
     """One comparison; returns the JSON record."""
     BETA[0] = beta

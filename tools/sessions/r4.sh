@@ -95,5 +95,38 @@ case "$1" in
     timeout -k 10 600 python -u -m pytest -v --timeout 500 --timeout-method thread \
         tests/test_gpu_arith_agreement.py tests/test_gpu_tolerance.py > $O/pytest_stationary.log 2>&1
     ;;
+  s4)
+    # config 2 with the k = 3 specialised speculative sweep: A/B against the
+    # generic-k variant (long launches, interleaved), one SQ pass per dtype;
+    # then the whole GPU suite (the stationary tests record their numbers)
+    # and the published line with its same-box profiles
+    V=ip_mcmc_amd/lib/variants/speck8/libipmc.so
+    SQS="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+    for i in 1 2; do
+      timeout -k 10 200 python tools/config_bench.py cfg2@16384 >> $O/l63_k3_ab.jsonl &&
+      IPMC_LIB_PATH=$V timeout -k 10 200 python tools/config_bench.py cfg2@16384 >> $O/l63_k3_ab.jsonl || exit 1
+    done &&
+    timeout -k 10 200 python tools/config_bench.py cfg2@16384:32 >> $O/l63_k3_ab.jsonl &&
+    timeout -s KILL 90 rocprofv3 --pmc $SQS --kernel-trace --output-format csv -d $O/sq_cfg2/f64 -o run -- \
+        python tools/config_bench.py cfg2@16384!f64 > /dev/null &&
+    timeout -s KILL 90 rocprofv3 --pmc $SQS --kernel-trace --output-format csv -d $O/sq_cfg2/f32 -o run -- \
+        python tools/config_bench.py cfg2@16384!f32 > /dev/null &&
+    python tools/sq_summarize.py $O/sq_cfg2/f64 small_spec_kernel > $O/sq_cfg2_f64.json &&
+    python tools/sq_summarize.py $O/sq_cfg2/f32 small_spec_kernel > $O/sq_cfg2_f32.json &&
+    { IPMC_RECORD_DIR=$O timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_s4.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; } &&
+    bash tools/sessions/r4.sh s2prof
+    ;;
+  s5)
+    # Lorenz-63 fp32 packing A/B at the sampler's launch length (s3's was at
+    # one step per launch: launch-bound), and the mixing-posterior small
+    # ensembles without speculation (spec width 1) beside s3's speculative rows
+    V=ip_mcmc_amd/lib/variants/l63scalar/libipmc.so
+    for i in 1 2; do
+      timeout -k 10 200 python tools/config_bench.py 'cfg2@16384!f32' >> $O/l63_pk_ab_long.jsonl &&
+      IPMC_LIB_PATH=$V timeout -k 10 200 python tools/config_bench.py 'cfg2@16384!f32' >> $O/l63_pk_ab_long.jsonl || exit 1
+    done &&
+    timeout -k 10 300 python tools/config_bench.py l96mx1~1@256 l96mx64~1@256 l96mx1024~1@256 >> $O/spec_mixing_nospec.jsonl
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
