@@ -327,7 +327,7 @@ __global__ void reg_add_kernel(int64_t n, int k, const T* __restrict__ u, const 
 }
 
 // ipmc_pcn_draws: one thread per (step, chain, component), grid-stride.  w is
-// formed with pcn_propose's / chol_propose's operations (draw_w, ipmc_rng.hpp:
+// formed with pcn_propose's / chol_noise's operations (draw_w, ipmc_rng.hpp:
 // the same bits as the sweep kernels' proposal noise and as the host
 // library's ipmc_host_pcn_draws); the j = 0 thread also writes log r.
 template <typename T>

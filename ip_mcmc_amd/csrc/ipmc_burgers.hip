@@ -433,10 +433,10 @@ constexpr int kBurQMax = 64;
 
 // S speculative slots of GS lanes per chain (S = 1: the sequential chain; S·GS
 // <= 64, or = kBurBlock: one chain per block, its slots on the block's waves,
-// combined through LDS): slot s evaluates step st+s from the current state as
-// if the steps before it in the round were rejected; the first accepting slot
-// ends the round -- or, for chains accepting most steps, along the accept path
-// (SpecRound, ipmc_sweep_common.hpp) -- bit-identical to S = 1.
+// combined through LDS): slot s is node s of the speculation tree for the
+// chain's recent acceptance rate (ipmc_spec_tree.hpp), and the chain walks the
+// tree along the real decisions (spec_walk, ipmc_sweep_common.hpp) --
+// bit-identical to S = 1.
 template <typename T, int CPL, int GS, bool FM>
 __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
   __shared__ T lds[kBurBlock * CPL];
@@ -463,36 +463,48 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
-  SpecGuess guess(spec_accept_prior(s, chain));  // the speculated path (ipmc_sweep_common.hpp)
+  SpecGuess guess(spec_accept_prior(s, chain));  // the speculation tree (ipmc_sweep_common.hpp)
   const bool rw = s.proposal == IPMC_PROPOSAL_RW;
   const T* chol = (const T*)s.prior_chol;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
-    const int64_t tt = st + slot;
-    const bool amode = S > 1 && guess.accept_mode();
+    const int tb = S > 1 ? guess.bucket() : 0;
+    const SpecNode nd = kSpecTrees.nd[tb][slot];
+    const int maxlvl = kSpecTrees.maxlvl[tb][S];
+    const bool act = nd.depth < left;  // uniform per slot
+    const int64_t tt = st + nd.depth;
+    const int og = nd.orig < 0 ? 0 : nd.orig;
     bool ok = false;
     T phv = (T)0;
     double lr = 0.0;
+    const uint64_t step = s.step0 + (uint64_t)tt;
+    T w[3];
+    if (act) pcn_noise<T, 3>(sq, s.seed, gid, step, 0, w, chol, 3);
+    const T bs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt] : beta;
+    const T cs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt + 1] : contr;
+    // the proposals level by level (every lane of a slot holds its proposal):
+    // a node's origin was formed one level before
     T v[3] = {(T)0, (T)0, (T)0};
-    if (slot < left) {  // uniform per slot
-      // the state this slot proposes from: the chain's, or (accept mode) the
-      // proposals of the slots before it, formed from their draws in step order
-      T pv[3] = {ur[0], ur[1], ur[2]};
-      if (amode) {
-        for (int q = 0; q < slot; ++q) {
-          const int64_t tq = st + q;
-          const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
-          const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
-          T nv[3];
-          pcn_propose<T, 3>(pv, sq, cq, bq, s.seed, gid, s.step0 + (uint64_t)tq, 0, nv, rw, chol, 3);
+    for (int lv = 0; lv <= maxlvl; ++lv) {
+      T o[3];
+      if (G <= 64) {
 #pragma unroll
-          for (int j = 0; j < 3; ++j) pv[j] = nv[j];
-        }
+        for (int j = 0; j < 3; ++j) o[j] = __shfl(v[j], cbase + og * GS, 64);
+      } else {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vpk[j][t] = v[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 3; ++j) o[j] = vpk[j][og * GS];
+        __syncthreads();
       }
-      const uint64_t step = s.step0 + (uint64_t)tt;
-      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
-      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      pcn_propose<T, 3>(pv, sq, cs, bs, s.seed, gid, step, 0, v, rw, chol, 3);
+      if (act && nd.lvl == lv) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] = propose_one<T>(rw, nd.orig < 0 ? ur[j] : o[j], w[j], cs, bs);
+      }
+    }
+    if (act) {  // uniform per slot
       ok = true;
       if (s.box_lo || s.box_hi) {
         const T* lo = (const T*)s.box_lo;
@@ -512,29 +524,36 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
         lr = det_log(accept_uniform(s.seed, gid, step));
       }
     }
-    // pcn_accept against the state this slot proposed from (accept mode: the
-    // previous slot's proposal, whose Φ its lanes hold)
-    T phl;
+    // pcn_accept against the state this node proposed from: the chain's, or
+    // its origin node's proposal (whose Φ that slot's lanes hold)
+    T pho;
     if (G <= 64) {
-      phl = __shfl(phv, cbase + (slot > 0 ? slot - 1 : 0) * GS, 64);
+      pho = __shfl(phv, cbase + og * GS, 64);
     } else {
       const int t = threadIdx.x;
 #pragma unroll
       for (int j = 0; j < 3; ++j) vpk[j][t] = v[j];
       vpk[3][t] = phv;
       __syncthreads();
-      phl = vpk[3][(slot > 0 ? slot - 1 : 0) * GS];
+      pho = vpk[3][og * GS];
     }
-    const bool acc = ok && (double)(((amode && slot > 0) ? phl : phu) - phv) > lr;
+    const bool acc = ok && (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
     // one bit per slot (its first lane, bit slot*GS of the chain's lanes)
+    const SpecNode* tree = kSpecTrees.nd[tb];
+    unsigned long long accm = 0, okm = 0;  // G <= 64: the chain's bits
+    const int kids = spec_pack_children(nd);
+    // G <= 64: node n's children from its slot's lanes; a block-wide chain: from the table
+    auto node = [&](int n) {
+      if (G <= 64) return spec_step_packed(__shfl(kids, cbase + n * GS, 64), n, GS, accm, okm);
+      const int bit = n * GS;
+      return spec_step_bits(tree, n, 0, bmask[0][bit >> 6] >> (bit & 63), bmask[1][bit >> 6] >> (bit & 63));
+    };
     SpecRound rd;
     T phf;
     if (G <= 64) {
-      const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
-      const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-      rd = spec_round(amode, accm, S, GS, left);
-      const int ubits = rd.used * GS;
-      ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+      accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
+      okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
+      rd = spec_walk(S, left, node, [](int, int) {});
       phf = __shfl(phv, cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
     } else {
       const int t = threadIdx.x;
@@ -544,51 +563,35 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
         bmask[1][t >> 6] = ob;
       }
       __syncthreads();
-      rd.first = S;  // the first slot whose guess failed
-      const int lim = left < S ? (int)left : S;
-      for (int w = kBurBlock / 64 - 1; w >= 0; --w) {
-        unsigned long long b = bmask[0][w];
-        if (amode) {  // the first rejection among the evaluated slots
-          unsigned long long ev = 0;
-          for (int i = 0; i < 64; i += GS)
-            if ((w * 64 + i) / GS < lim) ev |= 1ull << i;
-          b = ev & ~b;
-        }
-        if (b) rd.first = (w * 64 + __builtin_ctzll(b)) / GS;
-      }
-      rd.used = rd.first < S ? rd.first + 1 : lim;
-      rd.nar = amode ? (rd.first < S ? rd.first : lim) : (rd.first < S ? 1 : 0);
-      rd.win = amode ? rd.nar - 1 : (rd.first < S ? rd.first : -1);
-      const int ubits = rd.used * GS;
-#pragma unroll
-      for (int w = 0; w < kBurBlock / 64; ++w) {
-        const int nb = ubits - w * 64;
-        if (nb > 0) ncalls += __builtin_popcountll(bmask[1][w] & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
-      }
+      rd = spec_walk(S, left, node, [](int, int) {});
       phf = vpk[3][(rd.win >= 0 ? rd.win : 0) * GS];
     }
-    // the proposal of slot q (every lane of the chain runs this, uniform per chain)
+    if (G <= 64 && (s.sum_u || s.sample_every > 0)) {  // the recorded states read the parked proposals
+      const int t = threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) vpk[j][t] = v[j];
+      wave_sync_lds();
+    }
+    const int t0 = threadIdx.x - r;  // the chain's first thread in the block
+    // the proposal of slot q from the LDS park (every lane of the chain runs this, uniform per chain)
     auto slot_v = [&](int q, T (&out)[3]) {
-      if (G <= 64) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) out[j] = __shfl(v[j], cbase + q * GS, 64);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) out[j] = vpk[j][q * GS];
-      }
+      for (int j = 0; j < 3; ++j) out[j] = vpk[j][t0 + q * GS];
     };
     T vf[3];
-    slot_v(rd.win >= 0 ? rd.win : 0, vf);
-    if (s.sum_u || s.sample_every > 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
+    if (G > 64) slot_v(rd.win >= 0 ? rd.win : 0, vf);
+    if (s.sum_u || s.sample_every > 0) {  // uniform per chain (only lane r == 0 keeps the clock)
+      // the states after each settled step, in step order: the same walk again
       const bool sums = s.sum_u && r == 0;
       RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
                         sums ? 3 : 0);
-      for (int q = 0; q < rd.used; ++q) {
-        const int la = spec_last_acc(rd, amode, q);
+      spec_replay(rd.used, node, [&](int q, int la) {
         T vq[3];
         slot_v(la >= 0 ? la : 0, vq);
         if (r == 0) {
-          if (s.sum_u) {
+          if (sums) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
           }
@@ -600,16 +603,18 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
             for (int j = 0; j < 3; ++j) so[j] = la >= 0 ? vq[j] : ur[j];
           }
         }
-      }
+      });
       if (sums) rsum.store();
     }
     if (G > 64) __syncthreads();  // bmask / vpk are rewritten next round
+    else wave_sync_lds();
     if (rd.win >= 0) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) ur[j] = vf[j];
       phu = phf;
     }
     nacc += rd.nar;
+    ncalls += rd.calls;
     guess.settle(rd.nar, rd.used);
     st += rd.used;
   }

@@ -233,13 +233,12 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void
 
 // Speculative sweep for ensembles too small to fill the GPU (as
 // small_spec_kernel, ipmc_small.hpp): S slots of LPC lanes per chain
-// (S*LPC <= 64, one wavefront); slot s evaluates step st+s from the current
-// state -- exactly the proposal the sequential chain makes there if steps
-// st .. st+s-1 are rejected -- and the first accepting slot ends the round;
-// or, for chains accepting most steps, along the accept path (slot s proposes
-// from slot s-1's proposal, the first rejection ends the round; SpecRound in
-// ipmc_sweep_common.hpp).  The state lives in registers of every slot (ur)
-// and moves through the LDS park on acceptance.  Bit-identical to
+// (S*LPC <= 64, one wavefront, or one chain per block); slot s is node s of
+// the speculation tree for the chain's recent acceptance rate
+// (ipmc_spec_tree.hpp): it proposes step st + depth(s) from its origin node's
+// proposal (or the current state), and the chain walks the tree along the real
+// decisions (spec_walk, ipmc_sweep_common.hpp).  The state lives in registers
+// of every slot (ur) and the proposals in the LDS park.  Bit-identical to
 // l96_sweep_kernel.
 template <typename T, int D, int LPC, bool FM>
 __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m, const ipmc_sweep s, int S) {
@@ -274,42 +273,42 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
-  SpecGuess guess(spec_accept_prior(s, chain));  // the speculated path (ipmc_sweep_common.hpp)
+  SpecGuess guess(spec_accept_prior(s, chain));  // the speculation tree (ipmc_sweep_common.hpp)
+  const int lane0 = t - r + sub;  // slot 0's lane for my components
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
-    const int64_t tt = st + slot;
-    const bool amode = guess.accept_mode();
+    const int tb = guess.bucket();
+    const SpecNode nd = kSpecTrees.nd[tb][slot];
+    const int maxlvl = kSpecTrees.maxlvl[tb][S];
+    const bool act = nd.depth < left;  // uniform per slot: this node's step is in the launch
+    const int64_t tt = st + nd.depth;
+    const int og = nd.orig < 0 ? 0 : nd.orig;
     bool ok = false;
     T phv = (T)0;
     double lr = 0.0;
     int cl = c0;
     asm volatile("" : "+v"(cl));
-    if (slot < left) {  // uniform per slot
-      // the state this slot proposes from: the chain's, or (accept mode) the
-      // proposals of the slots before it, formed from their draws in step order
-      T pv[M];
+    const uint64_t step = s.step0 + (uint64_t)tt;
+    T w[M];
+    if (act) pcn_noise<T, M>((const T*)s.prior_sqrt + cl, s.seed, gid, step, c0, w, (const T*)s.prior_chol, D);
+    const T bs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt] : beta;
+    const T cs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt + 1] : contr;
+    // the proposals level by level: a node's origin was formed one level before
+    T v[M];
 #pragma unroll
-      for (int j = 0; j < M; ++j) pv[j] = ur[j];
-      if (amode) {
-        for (int q = 0; q < slot; ++q) {
-          const int64_t tq = st + q;
-          const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
-          const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
-          T nv[M];
-          pcn_propose<T, M>(pv, (const T*)s.prior_sqrt + cl, cq, bq, s.seed, gid, s.step0 + (uint64_t)tq, c0, nv, rw,
-                            (const T*)s.prior_chol, D);
+    for (int j = 0; j < M; ++j) v[j] = (T)0;
+    for (int lv = 0; lv <= maxlvl; ++lv) {
+      if (act && nd.lvl == lv) {
 #pragma unroll
-          for (int j = 0; j < M; ++j) pv[j] = nv[j];
+        for (int j = 0; j < M; ++j) {
+          v[j] = propose_one<T>(rw, nd.orig < 0 ? ur[j] : vpark[j][lane0 + og * LPC], w[j], cs, bs);
+          vpark[j][t] = v[j];
         }
       }
-      const uint64_t step = s.step0 + (uint64_t)tt;
-      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
-      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      T v[M];
-      pcn_propose<T, M>(pv, (const T*)s.prior_sqrt + cl, cs, bs, s.seed, gid, step, c0, v, rw,
-                        (const T*)s.prior_chol, D);
-#pragma unroll
-      for (int j = 0; j < M; ++j) vpark[j][t] = v[j];
+      if (G <= 64) wave_sync_lds();
+      else __syncthreads();
+    }
+    if (act) {  // uniform per slot
       ok = box_valid<T, M, LPC>(s, c0, v, lane);
       if (ok) {
         const T reg = s.reg_scale
@@ -321,27 +320,29 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
         lr = det_log(accept_uniform(s.seed, gid, step));
       }
     }
-    // pcn_accept against the state this slot proposed from (accept mode: the
-    // previous slot's proposal, whose Φ its lanes hold)
-    T phl;
+    // pcn_accept against the state this node proposed from: the chain's, or
+    // its origin node's proposal (whose Φ that slot's lanes hold)
+    T pho;
     if (G <= 64) {
-      phl = __shfl(phv, gbase + (slot > 0 ? slot - 1 : 0) * LPC, 64);
+      pho = __shfl(phv, gbase + og * LPC, 64);
     } else {
       phpark[t] = phv;
       __syncthreads();
-      phl = phpark[(slot > 0 ? slot - 1 : 0) * LPC];
+      pho = phpark[og * LPC];
     }
-    const bool acc = ok && (double)(((amode && slot > 0) ? phl : phu) - phv) > lr;
+    const bool acc = ok && (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
     // one bit per slot: the slot's lane sub == 0, at bit slot*LPC
     SpecRound rd;
     T phf;
+    unsigned long long accm = 0, okm = 0;  // G <= 64: the chain's bits
+    const SpecNode* tree = kSpecTrees.nd[tb];
     if (G <= 64) {
-      wave_sync_lds();
-      const unsigned long long accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
-      const unsigned long long okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
-      rd = spec_round(amode, accm, S, LPC, left);
-      const int ubits = rd.used * LPC;
-      ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
+      accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
+      okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
+      const int kids = spec_pack_children(nd);
+      rd = spec_walk(
+          S, left, [&](int n) { return spec_step_packed(__shfl(kids, gbase + n * LPC, 64), n, LPC, accm, okm); },
+          [](int, int) {});
       phf = __shfl(phv, gbase + (rd.win >= 0 ? rd.win : 0) * LPC, 64);
     } else {
       const unsigned long long ab = __ballot(acc && sub == 0), ob = __ballot(ok && sub == 0);
@@ -350,49 +351,40 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
         wmask[1][t >> 6] = ob;
       }
       __syncthreads();
-      rd.first = S;  // the first slot whose guess failed
-      const int lim = left < S ? (int)left : S;
-      for (int w = kL96Block / 64 - 1; w >= 0; --w) {
-        // slot bits of wave w: accept mode looks for the first rejection among the evaluated slots
-        unsigned long long b = wmask[0][w];
-        if (amode) {
-          unsigned long long ev = 0;
-          for (int i = 0; i < 64; i += LPC)
-            if ((w * 64 + i) / LPC < lim) ev |= 1ull << i;
-          b = ev & ~b;
-        }
-        if (b) rd.first = (w * 64 + __builtin_ctzll(b)) / LPC;
-      }
-      rd.used = rd.first < S ? rd.first + 1 : lim;
-      rd.nar = amode ? (rd.first < S ? rd.first : lim) : (rd.first < S ? 1 : 0);
-      rd.win = amode ? rd.nar - 1 : (rd.first < S ? rd.first : -1);
-      const int ubits = rd.used * LPC;  // the lanes of the used slots: bits [0, ubits) of the block
-#pragma unroll
-      for (int w = 0; w < kL96Block / 64; ++w) {
-        const int nb = ubits - w * 64;
-        if (nb > 0) ncalls += __builtin_popcountll(wmask[1][w] & (nb >= 64 ? ~0ull : ((1ull << nb) - 1)));
-      }
+      rd = spec_walk(
+          S, left,
+          [&](int n) {
+            const int bit = n * LPC;
+            return spec_step_bits(tree, n, 0, wmask[0][bit >> 6] >> (bit & 63), wmask[1][bit >> 6] >> (bit & 63));
+          },
+          [](int, int) {});
       phf = phpark[(rd.win >= 0 ? rd.win : 0) * LPC];
     }
-    const int lane0 = t - r + sub;  // slot 0's lane for my components
-    if (s.sum_u && slot == 0) {
-      RoundSums<M> rsum(s.sum_u + chain * D + c0, s.sum_u2 ? s.sum_u2 + chain * D + c0 : nullptr, M);
-      for (int q = 0; q < rd.used; ++q) {
-        const int la = spec_last_acc(rd, amode, q);
+    if (slot == 0 && (s.sum_u || (s.sample_every > 0 && clk.next < st + rd.used))) {
+      // the states after each settled step, in step order: the same walk again
+      const bool sums = s.sum_u != nullptr;
+      RoundSums<M> rsum(sums ? s.sum_u + chain * D + c0 : nullptr,
+                        (sums && s.sum_u2) ? s.sum_u2 + chain * D + c0 : nullptr, sums ? M : 0);
+      spec_replay(
+          rd.used,
+          [&](int n) {
+            if (G <= 64) return spec_step_bits(tree, n, LPC, accm, okm);
+            const int bit = n * LPC;
+            return spec_step_bits(tree, n, 0, wmask[0][bit >> 6] >> (bit & 63), wmask[1][bit >> 6] >> (bit & 63));
+          },
+          [&](int q, int la) {
+            if (sums) {
 #pragma unroll
-        for (int j = 0; j < M; ++j) rsum.add(j, la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j]);
-      }
-      rsum.store();
-    }
-    if (s.sample_every > 0 && slot == 0) {
-      // the samples among the `used` steps: the state after step st+q
-      while (clk.next < st + rd.used) {
-        const int la = spec_last_acc(rd, amode, (int)(clk.next - st));
-        const int64_t sl = clk.take(clk.next);
-        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
+              for (int j = 0; j < M; ++j) rsum.add(j, la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j]);
+            }
+            if (s.sample_every > 0 && clk.next == st + q) {
+              const int64_t sl = clk.take(clk.next);
+              T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
 #pragma unroll
-        for (int j = 0; j < M; ++j) so[j] = la >= 0 ? vpark[j][lane0 + la * LPC] : ur[j];
-      }
+              for (int j = 0; j < M; ++j) so[j] = la >= 0 ? vpark[j][lane0 + la * LPC] : ur[j];
+            }
+          });
+      if (sums) rsum.store();
     }
     if (rd.win >= 0) {
 #pragma unroll
@@ -400,6 +392,7 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
       phu = phf;
     }
     nacc += rd.nar;
+    ncalls += rd.calls;
     guess.settle(rd.nar, rd.used);
     if (G <= 64) wave_sync_lds();  // the parks are rewritten next round
     else __syncthreads();

@@ -485,10 +485,10 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
 }
 
 // Sweep with S speculative slots per chain (S = 1: the plain sequential chain).
-// A chain owns S consecutive groups of L = K/SPL lanes; slot s evaluates step
-// st+s from the current state as if the steps before it in the round were
-// rejected, and the first accepting slot ends the round (see
-// small_spec_kernel) -- bit-identical to S = 1.  ⌊64 / (S·L)⌋ chains per wave.
+// A chain owns S consecutive groups of L = K/SPL lanes; slot s is node s of
+// the speculation tree for the chain's recent acceptance rate (see
+// small_spec_kernel, ipmc_spec_tree.hpp) -- bit-identical to S = 1.
+// ⌊64 / (S·L)⌋ chains per wave.
 template <typename T, int J, bool FM, int SPL>
 __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep_kernel(const ipmc_model m,
                                                                                       const ipmc_sweep s, int S) {
@@ -512,37 +512,40 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
   int nacc = 0, ncalls = 0;
   SampleClock clk(s);
   int64_t st = 0;
-  SpecGuess guess(spec_accept_prior(s, chain));
+  SpecGuess guess(spec_accept_prior(s, chain));  // the speculation tree (ipmc_sweep_common.hpp)
   const T* chol = (const T*)s.prior_chol;
+  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
-    const int64_t tt = st + slot;
-    const bool amode = S > 1 && guess.accept_mode();
+    const int tb = S > 1 ? guess.bucket() : 0;
+    const SpecNode nd = kSpecTrees.nd[tb][slot];
+    const int maxlvl = kSpecTrees.maxlvl[tb][S];
+    const bool act = nd.depth < left;  // uniform per slot
+    const int64_t tt = st + nd.depth;
+    const int ol = cbase + (nd.orig < 0 ? 0 : nd.orig) * L;  // the origin slot's first lane
     int kq = c.sub;
     asm volatile("" : "+v"(kq));
     bool ok = false, acc = false;
     T phv = (T)0;
     double lr = 0.0;
+    const uint64_t step = s.step0 + (uint64_t)tt;
+    T w[3];
+    if (act) pcn_noise<T, 3>(sq, s.seed, gid, step, 0, w, chol, 3);
+    const T bs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt] : beta;
+    const T cs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt + 1] : contr;
+    // the proposals level by level (every lane of a slot holds its proposal):
+    // a node's origin was formed one level before
     T v[3] = {(T)0, (T)0, (T)0};
-    if (slot < left) {  // uniform per slot
-      // the state this slot proposes from: the chain's, or (accept mode) the
-      // proposals of the slots before it, formed from their draws in step order
-      T pv[3] = {ur[0], ur[1], ur[2]};
-      if (amode) {
-        for (int q = 0; q < slot; ++q) {
-          const int64_t tq = st + q;
-          const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
-          const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
-          T nv[3];
-          pcn_propose<T, 3>(pv, sq, cq, bq, s.seed, gid, s.step0 + (uint64_t)tq, 0, nv, rw, chol, 3);
+    for (int lv = 0; lv <= maxlvl; ++lv) {
+      T o[3];
 #pragma unroll
-          for (int j = 0; j < 3; ++j) pv[j] = nv[j];
-        }
+      for (int j = 0; j < 3; ++j) o[j] = __shfl(v[j], ol, 64);
+      if (act && nd.lvl == lv) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] = propose_one<T>(rw, nd.orig < 0 ? ur[j] : o[j], w[j], cs, bs);
       }
-      const uint64_t step = s.step0 + (uint64_t)tt;
-      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
-      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
-      pcn_propose<T, 3>(pv, sq, cs, bs, s.seed, gid, step, 0, v, rw, chol, 3);
+    }
+    if (act) {  // uniform per slot
       ok = true;
       if (s.box_lo || s.box_hi) {
         const T* lo = (const T*)s.box_lo;
@@ -561,67 +564,49 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
         lr = det_log(accept_uniform(s.seed, gid, step));
       }
     }
-    // pcn_accept against the state this slot proposed from (accept mode: the
-    // previous slot's proposal, whose Φ its lanes hold)
-    const T phl = __shfl(phv, cbase + (slot > 0 ? slot - 1 : 0) * L, 64);
-    if (ok) acc = (double)(((amode && slot > 0) ? phl : phu) - phv) > lr;
+    // pcn_accept against the state this node proposed from: the chain's, or
+    // its origin node's proposal (whose Φ that slot's lanes hold)
+    const T pho = __shfl(phv, ol, 64);
+    if (ok) acc = (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
     // one bit per slot (its first lane, at bit slot*L of the chain's lanes)
-    const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1);
     const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
     const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-    const SpecRound rd = spec_round(amode, accm, S, L, left);
-    const int ubits = rd.used * L;
-    ncalls += __builtin_popcountll(okm & (ubits >= 64 ? ~0ull : ((1ull << ubits) - 1)));
-    // every slot's proposal is needed for the recorded states of an accept-mode round
-    const int wl = cbase + (rd.win >= 0 ? rd.win : 0) * L;  // the winning slot's first lane
+    const int kids = spec_pack_children(nd);
+    const SpecRound rd = spec_walk(
+        S, left, [&](int n) { return spec_step_packed(__shfl(kids, cbase + n * L, 64), n, L, accm, okm); },
+        [](int, int) {});
+    const int wl = cbase + (rd.win >= 0 ? rd.win : 0) * L;  // the new state's slot, first lane
     T vf[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
     const T phf = __shfl(phv, wl, 64);
-    const bool sums = s.sum_u && r == 0;
-    if ((s.sum_u || s.sample_every > 0) && amode) {
-      // recorded states of an accept-mode round: slot q's proposal for q < nar,
-      // gathered by every lane (uniform loop), written by lane r == 0
+    if (s.sum_u || s.sample_every > 0) {  // uniform per chain (only lane r == 0 keeps the clock)
+      // the states after each settled step, in step order: the same walk again,
+      // gathered by every lane of the chain (uniform per chain), written by lane r == 0
+      const bool sums = s.sum_u && r == 0;
       RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
                         sums ? 3 : 0);
-      for (int q = 0; q < rd.used; ++q) {
-        const int la = spec_last_acc(rd, amode, q);
-        T vq[3];
+      const SpecNode* tree = kSpecTrees.nd[tb];
+      spec_replay(
+          rd.used, [&](int n) { return spec_step_bits(tree, n, L, accm, okm); },
+          [&](int q, int la) {
+            T vq[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * L, 64);
-        if (r == 0) {
-          if (s.sum_u) {
+            for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * L, 64);
+            if (r == 0) {
+              if (sums) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
-          }
-          if (s.sample_every > 0 && clk.next == st + q) {
-            const int64_t sl = clk.take(clk.next);
-            T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+                for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
+              }
+              if (s.sample_every > 0 && clk.next == st + q) {
+                const int64_t sl = clk.take(clk.next);
+                T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) so[j] = la >= 0 ? vq[j] : ur[j];
-          }
-        }
-      }
+                for (int j = 0; j < 3; ++j) so[j] = la >= 0 ? vq[j] : ur[j];
+              }
+            }
+          });
       if (sums) rsum.store();
-    } else {
-      if (sums) {
-        RoundSums<3> rsum(s.sum_u + chain * 3, s.sum_u2 ? s.sum_u2 + chain * 3 : nullptr, 3);
-        for (int qq = 0; qq < rd.used; ++qq) {
-#pragma unroll
-          for (int j = 0; j < 3; ++j) rsum.add(j, (qq == rd.first) ? (double)vf[j] : (double)ur[j]);
-        }
-        rsum.store();
-      }
-      if (s.sample_every > 0 && r == 0) {
-        // the samples among the `used` steps: the state after step st+qq
-        while (clk.next < st + rd.used) {
-          const int qq = (int)(clk.next - st);
-          const int64_t sl = clk.take(clk.next);
-          T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) so[j] = (qq == rd.first) ? vf[j] : ur[j];
-        }
-      }
     }
     if (rd.win >= 0) {
 #pragma unroll
@@ -629,6 +614,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
       phu = phf;
     }
     nacc += rd.nar;
+    ncalls += rd.calls;
     guess.settle(rd.nar, rd.used);
     st += rd.used;
   }

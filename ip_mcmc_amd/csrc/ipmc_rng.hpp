@@ -11,7 +11,7 @@
 //    (DESIGN.md §4).  Both compilers run with -ffp-contract=off, so nothing is
 //    fused.
 //  * draw_w: one component of a step's proposal noise, sqrt(C_jj)·ξ_j or
-//    Σ_{i<=j} L_ji ξ_i (chol_propose's order) -- ipmc_pcn_draws' element.
+//    Σ_{i<=j} L_ji ξ_i (chol_noise's order) -- ipmc_pcn_draws' element.
 #pragma once
 
 #include <stdint.h>
@@ -157,7 +157,7 @@ IPMC_HD double accept_uniform(uint64_t seed, uint64_t chain, uint64_t step) {
 
 // Component j of the proposal noise w of (chain gid, step): sqrt(C_jj)·ξ_j
 // for a diagonal prior (sq), else Σ_{i<=j} L_ji ξ_i summed in ascending i
-// from +0 with no FMA (chol_propose / oracle/orc_models.inc: the same order),
+// from +0 with no FMA (chol_noise / oracle/orc_models.inc: the same order),
 // in the chain dtype T.
 template <typename T>
 IPMC_HD T draw_w(uint64_t seed, uint64_t gid, uint64_t step, int j, int k, const T* sq, const T* chol) {

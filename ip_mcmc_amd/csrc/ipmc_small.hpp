@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
     double z0 = 0.0, z1 = 0.0;
     bool ok = true;
     if (chol) {
-      // non-diagonal prior (chol_propose's order): ξ parked first, then
+      // non-diagonal prior (chol_noise's order): ξ parked first, then
       // w_j = Σ_{i<=j} L[j][i] ξ_i for descending j, each v_j replacing ξ_j
       for (int j = 0; j < k; j += 2) {
         normal_pair(s.seed, gid, step, (uint32_t)(j >> 1), z0, z1);
@@ -257,14 +257,15 @@ __global__ __launch_bounds__(kSmallBlock) void small_sweep_kernel(const ipmc_mod
 
 // ------------------------------------------------------------ speculation
 // Small ensembles leave most of the GPU idle and a chain's steps are a
-// latency-bound sequence.  With S lanes per chain, lane s evaluates the step
-// st + s as if steps st .. st+s-1 were all rejected: its proposal is drawn
-// from the current state with the counter-based draws of step st + s, so it
-// is exactly the proposal the sequential chain makes if it gets there.  The
-// first lane whose proposal is accepted ends the round (later lanes' work is
-// discarded and redone from the new state), so u, Φ, the counters, the sums
-// and the samples are bit-identical to the one-lane kernel; a round advances
-// the chain by up to S steps in one forward-map latency.
+// latency-bound sequence.  With S lanes per chain, lane s is node s of a
+// speculation tree (ipmc_spec_tree.hpp): it evaluates step st + depth(s) from
+// the proposal of its origin node (or the current state) with the
+// counter-based draws of that step, so it is exactly the proposal the
+// sequential chain makes if the decisions before it go the node's way.  The
+// chain walks the tree along the real decisions (the nodes off its path are
+// discarded and redone), so u, Φ, the counters, the sums and the samples are
+// bit-identical to the one-lane kernel; a round advances the chain by up to S
+// steps in about one forward-map latency.
 // gfx950 only: the f64 linear kernel's LDS (small_spec_lds_bytes) is 96 KiB at
 // the default 256 threads, static_assert'ed against kLdsBytesPerCU.
 #ifndef IPMC_SPEC_BLOCK  // block-size experiments (tools/build_variant.sh)
@@ -306,14 +307,14 @@ constexpr int kPreFactor = 4;
 constexpr int kPreLds = kPreFactor * kSpecBlock;  // steps per block (all groups)
 
 // LDS of one small_spec_kernel block: the proposal park, the linear model's
-// constants and (linear) the pre-drawn w / log r, (others) the slots' w.  f64 at kSpecBlock = 256 is
+// constants and (linear) the pre-drawn w / log r.  f64 at kSpecBlock = 256 is
 // 96 KiB -- it fits gfx950's 160 KiB per CU only (64 KiB on gfx942): a larger
 // IPMC_SPEC_BLOCK or kPreFactor has to stay under the limit.
 template <typename T, int MODEL>
 constexpr size_t small_spec_lds_bytes() {
   return sizeof(T) * (size_t)kSpecKMax * kSpecBlock + sizeof(T) * (MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1) +
-         (MODEL == IPMC_MODEL_LINEAR ? (sizeof(T) * (size_t)kPreLds * kSpecKMax + sizeof(double) * kPreLds + sizeof(T))
-                                     : sizeof(T) + sizeof(double) + sizeof(T) * (size_t)kSpecKMax * kSpecBlock);
+         (MODEL == IPMC_MODEL_LINEAR ? (sizeof(T) * (size_t)kPreLds * kSpecKMax + sizeof(double) * kPreLds)
+                                     : sizeof(T) + sizeof(double));
 }
 
 template <typename T, int MODEL, bool FM, int S>
@@ -326,7 +327,6 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   __shared__ T lin_c[MODEL == IPMC_MODEL_LINEAR ? kSpecLinLds : 1];
   __shared__ T pre_w[PRE ? kPreLds * kSpecKMax : 1];    // [group][step in chunk][j]
   __shared__ double pre_lr[PRE ? kPreLds : 1];           // [group][step in chunk]: log r
-  __shared__ T wpark[PRE ? 1 : kSpecKMax * kSpecBlock];  // accept mode: the slots' w (non-PRE)
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int sub = t & (S - 1);
@@ -413,25 +413,20 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
       }
     }
   };
-  // The speculated path (results are bit-identical either way; only the steps
-  // a round settles change).  Reject mode: every slot proposes from the
-  // current state -- the path on which the next steps are rejected -- and the
-  // first acceptance ends the round.  Accept mode: slot s proposes from slot
-  // s-1's proposal -- the path on which they are accepted, each slot forming
-  // the proposals of the slots before it from their draws in the sequential
-  // order -- and the first rejection ends the round; the mismatching slot's own
-  // decision is valid (its inputs were right), so a round settles up to S
-  // steps either way.  A chain runs accept mode while it accepted at least half
-  // of its recent steps (SpecGuess; at its first round: its accept counter over
-  // the global steps before the launch, if any).  Config 2 accepts 88 %: reject
-  // mode settles ~1.1 steps per round there, accept mode ~1/(1-p) = 8.
+  // The speculation tree (ipmc_sweep_common.hpp, ipmc_spec_tree.hpp): lane
+  // `sub` of the group is node `sub` of the tree for the chain's recent
+  // acceptance rate; its proposal starts from its origin node's, formed one
+  // level earlier.  Config 2 accepts 88 %: the tree there is the accept chain
+  // (~7 steps per round at S = 16); a chain accepting nothing gets the reject
+  // chain (S steps per round).
   SpecGuess guess(spec_accept_prior(s, chain));
-  T* wown = wpark + t;                    // this lane's proposal noise, wown[j * kSpecBlock] (accept mode)
-  const T* wgroup = wpark + (t - sub);
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
-    const int64_t tt = st + sub;
-    const bool amode = guess.accept_mode();
+    const int tb = guess.bucket();
+    const SpecNode nd = kSpecTrees.nd[tb][sub];
+    const int maxlvl = kSpecTrees.maxlvl[tb][S];
+    const bool act = nd.depth < left;  // this node's step is in the launch
+    const int64_t tt = st + nd.depth;
     if constexpr (PRE) {
       // refill when this round's slots reach past the held draws (uniform per group)
       if (st + S > pend && pend < s.n_steps) {
@@ -454,56 +449,45 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
         wave_sync_lds();
       }
     }
-    // this slot's proposal noise w (step tt)
+    // this node's proposal noise w (step tt)
     T w[KM];
-    if (sub < left) {
+    if (act) {
       if constexpr (PRE) {
         const int pi = (int)(tt - pbase);
 #pragma unroll
         for (int j = 0; j < KM; ++j) w[j] = gw[pi * KM + j];
       } else {
         draw_w(s.step0 + (uint64_t)tt, w);
-        if (amode) {
-#pragma unroll
-          for (int j = 0; j < KM; ++j) wown[j * kSpecBlock] = w[j];
-        }
       }
     }
-    // accept mode: the proposals of the slots before this one, in step order
-    T pv[KM];
+    const T bs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt] : beta;
+    const T cs = (act && s.beta_schedule) ? (T)s.beta_schedule[2 * tt + 1] : contr;
+    // the proposals level by level: a node's origin was formed one level before
+    T vr[KM];
 #pragma unroll
-    for (int j = 0; j < KM; ++j) pv[j] = ur[j];
-    if (!PRE) wave_sync_lds();  // the parked w of the group's slots
-    if (amode) {
-      const int64_t lim = left < S ? left : S;
-#pragma unroll 1
-      for (int q = 0; q < sub && q < lim; ++q) {
-        const int64_t tq = st + q;
-        const T bq = s.beta_schedule ? (T)s.beta_schedule[2 * tq] : beta;
-        const T cq = s.beta_schedule ? (T)s.beta_schedule[2 * tq + 1] : contr;
+    for (int j = 0; j < KM; ++j) vr[j] = (T)0;
+    for (int lv = 0; lv <= maxlvl; ++lv) {
+      if (act && nd.lvl == lv) {
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
           if (j < k) {
-            const T wq = PRE ? gw[(int)(tq - pbase) * KM + j] : wgroup[j * kSpecBlock + q];
-            pv[j] = propose_one<T>(rw, pv[j], wq, cq, bq);
+            const T o = nd.orig < 0 ? ur[j] : vgroup[j * kSpecBlock + nd.orig];
+            vr[j] = propose_one<T>(rw, o, w[j], cs, bs);
+            v[j * kSpecBlock] = vr[j];
           }
         }
       }
+      wave_sync_lds();
     }
     bool ok = false, acc = false;
     T phv = (T)0;
     double lr = 0.0;
-    if (sub < left) {
-      const uint64_t step = s.step0 + (uint64_t)tt;
-      const T bs = s.beta_schedule ? (T)s.beta_schedule[2 * tt] : beta;
-      const T cs = s.beta_schedule ? (T)s.beta_schedule[2 * tt + 1] : contr;
+    if (act) {
       ok = true;
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
         if (j < k) {
-          const T vj = propose_one<T>(rw, pv[j], w[j], cs, bs);
-          v[j * kSpecBlock] = vj;
-          const T tb = vj + offr[j];  // + 0 when there is no offset: the same bits as vj
+          const T tb = vr[j] + offr[j];  // + 0 when there is no offset: the same bits as v_j
           if (lo && !(lor[j] < tb)) ok = false;
           if (hi && !(tb < hir[j])) ok = false;
         }
@@ -527,66 +511,54 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
           }
           phv = phv + (T)0.5 * r2;
         }
-        lr = PRE ? glr[tt - pbase] : det_log(accept_uniform(s.seed, gid, step));
+        lr = PRE ? glr[tt - pbase] : det_log(accept_uniform(s.seed, gid, s.step0 + (uint64_t)tt));
       }
     }
-    // pcn_accept against the state this slot proposed from: the current state,
-    // or (accept mode) the previous slot's proposal
-    const T phl = __shfl(phv, (lane + 63) & 63, 64);
-    if (ok) acc = (double)(((amode && sub > 0) ? phl : phu) - phv) > lr;
-    wave_sync_lds();
+    // pcn_accept against the state this node proposed from: the chain's, or its origin node's proposal
+    const T pho = __shfl(phv, gbase + (nd.orig < 0 ? 0 : nd.orig), 64);
+    if (ok) acc = (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
     const unsigned long long accm = (__ballot(acc) >> gbase) & gmask;
     const unsigned long long okm = (__ballot(ok) >> gbase) & gmask;
-    const int lim = (int)(left < S ? left : S);
-    int first, used, nar, win;  // first mismatching slot, steps settled, accepts, slot of the new state
-    if (!amode) {
-      first = accm ? __builtin_ctzll(accm) : S;  // first accepted slot of the group
-      used = first < S ? first + 1 : lim;
-      nar = first < S ? 1 : 0;
-      win = first < S ? first : -1;
-    } else {
-      const unsigned long long rej = ~accm & (lim >= 64 ? ~0ull : ((1ull << lim) - 1));
-      first = rej ? __builtin_ctzll(rej) : S;  // first rejected slot
-      used = first < S ? first + 1 : lim;
-      nar = first < S ? first : lim;
-      win = nar - 1;
-    }
-    ncalls += __builtin_popcountll(okm & (used >= 64 ? ~0ull : ((1ull << used) - 1)));
-    const T phf = __shfl(phv, gbase + (win >= 0 ? win : 0), 64);
-    // the slot whose proposal is the state after step st+q (-1: the old state)
-    auto last_acc = [&](int q) { return amode ? (q < nar ? q : nar - 1) : (q == first ? first : -1); };
-    if (s.sum_u && sub == 0) {
-      // the states after each of the `used` steps, in step order
-      RoundSums<KM> rsum(s.sum_u + chain * k, s.sum_u2 ? s.sum_u2 + chain * k : nullptr, k);
-      for (int q = 0; q < used; ++q) {
-        const int la = last_acc(q);
+    const int kids = spec_pack_children(nd);
+    const SpecRound rd = spec_walk(
+        S, left,
+        [&](int n) { return spec_step_packed(__shfl(kids, gbase + n, 64), n, 1, accm, okm); },
+        [](int, int) {});
+    const T phf = __shfl(phv, gbase + (rd.win >= 0 ? rd.win : 0), 64);
+    if (sub == 0 && (s.sum_u || (s.sample_every > 0 && clk.next < st + rd.used))) {
+      // the states after each settled step, in step order: the same walk again
+      const bool sums = s.sum_u != nullptr;
+      RoundSums<KM> rsum(sums ? s.sum_u + chain * k : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * k : nullptr,
+                         sums ? k : 0);
+      const SpecNode* tree = kSpecTrees.nd[tb];
+      spec_replay(rd.used, [&](int n) { return spec_step_bits(tree, n, 1, accm, okm); },
+                  [&](int q, int la) {
+                  if (sums) {
 #pragma unroll
-        for (int j = 0; j < KM; ++j)
-          if (j < k) rsum.add(j, la >= 0 ? (double)vgroup[j * kSpecBlock + la] : (double)ur[j]);
-      }
-      rsum.store();
-    }
-    if (s.sample_every > 0 && sub == 0) {
-      // the samples among the `used` steps: the state after step st+q
-      while (clk.next < st + used) {
-        const int la = last_acc((int)(clk.next - st));
-        const int64_t sl = clk.take(clk.next);
-        T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
+                    for (int j = 0; j < KM; ++j)
+                      if (j < k) rsum.add(j, la >= 0 ? (double)vgroup[j * kSpecBlock + la] : (double)ur[j]);
+                  }
+                  if (s.sample_every > 0 && clk.next == st + q) {
+                    const int64_t sl = clk.take(clk.next);
+                    T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride;
 #pragma unroll
-        for (int j = 0; j < KM; ++j)
-          if (j < k) so[j] = la >= 0 ? vgroup[j * kSpecBlock + la] : ur[j];
-      }
+                    for (int j = 0; j < KM; ++j)
+                      if (j < k) so[j] = la >= 0 ? vgroup[j * kSpecBlock + la] : ur[j];
+                  }
+                });
+      if (sums) rsum.store();
     }
-    if (win >= 0) {
+    if (rd.win >= 0) {
 #pragma unroll
       for (int j = 0; j < KM; ++j)
-        if (j < k) ur[j] = vgroup[j * kSpecBlock + win];
+        if (j < k) ur[j] = vgroup[j * kSpecBlock + rd.win];
       phu = phf;
     }
-    nacc += nar;
-    guess.settle(nar, used);
+    nacc += rd.nar;
+    ncalls += rd.calls;
+    guess.settle(rd.nar, rd.used);
     wave_sync_lds();  // the parks are rewritten next round
-    st += used;
+    st += rd.used;
   }
   if (sub == 0) {
     phi[chain] = phu;

@@ -8,6 +8,7 @@
 
 #include "../../include/ipmc.h"
 #include "ipmc_device.hpp"
+#include "ipmc_spec_tree.hpp"
 
 namespace ipmc {
 
@@ -25,10 +26,8 @@ __device__ __forceinline__ T propose_one(bool rw, T u, T w, T contr, T beta) {
 // owning components [c0, c0+M) draws ξ_0 .. ξ_{c0+M-1} itself (the proposal is
 // a negligible part of a step next to G).
 template <typename T, int M>
-__device__ __forceinline__ void chol_propose(const T* __restrict__ u, const T* __restrict__ L, int k, T contr,
-                                             T beta, uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M],
-                                             bool rw) {
-  T w[M];
+__device__ __forceinline__ void chol_noise(const T* __restrict__ L, int k, uint64_t seed, uint64_t gid, uint64_t step,
+                                           int c0, T (&w)[M]) {
 #pragma unroll
   for (int j = 0; j < M; ++j) w[j] = (T)0;
   const int iend = c0 + M;
@@ -43,16 +42,15 @@ __device__ __forceinline__ void chol_propose(const T* __restrict__ u, const T* _
       if (i + 1 <= r) w[j] = w[j] + x1 * L[(int64_t)r * k + i + 1];
     }
   }
-#pragma unroll
-  for (int j = 0; j < M; ++j) v[j] = propose_one<T>(rw, u[j], w[j], contr, beta);
 }
 
+// A step's proposal noise w for components [c0, c0+M): sqrt(C_jj)·ξ_j, or
+// Σ_{i<=j} L_ji ξ_i with a Cholesky factor.
 template <typename T, int M>
-__device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __restrict__ sq, T contr, T beta,
-                                            uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M],
-                                            bool rw = false, const T* __restrict__ chol = nullptr, int k = 0) {
+__device__ __forceinline__ void pcn_noise(const T* __restrict__ sq, uint64_t seed, uint64_t gid, uint64_t step, int c0,
+                                          T (&w)[M], const T* __restrict__ chol = nullptr, int k = 0) {
   if (chol) {
-    chol_propose<T, M>(u, chol, k, contr, beta, seed, gid, step, c0, v, rw);
+    chol_noise<T, M>(chol, k, seed, gid, step, c0, w);
     return;
   }
   if constexpr (M % 2 == 0) {
@@ -61,10 +59,8 @@ __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __
     for (int j = 0; j < M; j += 2) {
       double z0, z1;
       normal_pair(seed, gid, step, (uint32_t)((c0 + j) >> 1), z0, z1);
-      const T w0 = sq[j] * (T)z0;
-      const T w1 = sq[j + 1] * (T)z1;
-      v[j] = propose_one<T>(rw, u[j], w0, contr, beta);
-      v[j + 1] = propose_one<T>(rw, u[j + 1], w1, contr, beta);
+      w[j] = sq[j] * (T)z0;
+      w[j + 1] = sq[j + 1] * (T)z1;
     }
   } else {
     double z0 = 0.0, z1 = 0.0;
@@ -72,10 +68,19 @@ __device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __
     for (int j = 0; j < M; ++j) {
       const int c = c0 + j;
       if (j == 0 || (c & 1) == 0) normal_pair(seed, gid, step, (uint32_t)(c >> 1), z0, z1);
-      const T w = sq[j] * (T)((c & 1) ? z1 : z0);
-      v[j] = propose_one<T>(rw, u[j], w, contr, beta);
+      w[j] = sq[j] * (T)((c & 1) ? z1 : z0);
     }
   }
+}
+
+template <typename T, int M>
+__device__ __forceinline__ void pcn_propose(const T* __restrict__ u, const T* __restrict__ sq, T contr, T beta,
+                                            uint64_t seed, uint64_t gid, uint64_t step, int c0, T (&v)[M],
+                                            bool rw = false, const T* __restrict__ chol = nullptr, int k = 0) {
+  T w[M];
+  pcn_noise<T, M>(sq, seed, gid, step, c0, w, chol, k);
+#pragma unroll
+  for (int j = 0; j < M; ++j) v[j] = propose_one<T>(rw, u[j], w[j], contr, beta);
 }
 
 // s = Σ_i r_i^2 over the chain's q = LPC*M residuals in component order
@@ -177,28 +182,42 @@ struct SampleClock {
 };
 
 // ---------------------------------------------------------- speculation
-// A speculative round evaluates the next S steps of a chain at once, slot s
-// taking step st+s under a guess of the decisions before it: reject mode (the
-// steps before it rejected: every slot proposes from the current state, the
-// first acceptance ends the round) or accept mode (accepted: slot s proposes
-// from slot s-1's proposal, the first rejection ends the round).  The slot
-// where the guess first fails still decided correctly (its inputs were
-// right), so a round settles `used` steps either way and the results are
-// bit-identical to the sequential chain; the guess only changes how many.
-// A chain guesses "accept" while it accepted at least half of its recent
-// steps: accepted and settled steps summed over its rounds with weight 3/4 per
-// round back (~4 rounds).  Rounds 1-3 used the whole launch's ratio, which
-// lags behind a posterior whose acceptance changes along the run (burn-in, a
-// step-size schedule) once launches are long (sampler.STEPS_PER_LAUNCH).
-// Before its first round: `prior`.
+// A speculative round evaluates several future steps of a chain at once, its
+// S slots taking the first S nodes of a speculation tree (ipmc_spec_tree.hpp):
+// node n proposes step st + depth(n) from the proposal of its origin node (or
+// the chain's state) with that step's draws, so it is exactly the proposal
+// the sequential chain makes there if the decisions before it go the way the
+// node's path says.  The chain then walks the tree along the real decisions
+// (spec_walk): every visited node's decision is the sequential chain's, and
+// the round settles the steps up to the first node whose next node is not
+// among the slots.  Results are bit-identical to the sequential chain for any
+// tree; the tree, picked by the chain's recent acceptance rate, only sets how
+// many steps a round settles.
+static __constant__ const SpecTrees kSpecTrees = make_spec_trees();
+
+#ifndef IPMC_SPEC_TREE  // 0: rounds 3-4's two paths only, reject or accept chain (A/B)
+#define IPMC_SPEC_TREE 1
+#endif
+
+// The chain's recent acceptance rate: accepted and settled steps summed over
+// its rounds with weight 3/4 per round back (~4 rounds).  Rounds 1-3 used the
+// whole launch's ratio, which lags behind a posterior whose acceptance changes
+// along the run (burn-in, a step-size schedule) once launches are long
+// (sampler.STEPS_PER_LAUNCH).  Before its first round: `prior`.
 struct SpecGuess {
   float a, n;  // recency-weighted accepted / settled steps
-  __device__ __forceinline__ explicit SpecGuess(bool prior) : a(prior ? 1.f : 0.f), n(1.f) {}
-  __device__ __forceinline__ bool accept_mode() const {
-#ifdef IPMC_SPEC_REJECT_ONLY  // experiments (tools/build_variant.sh): the reject path only
-    return false;
+  __device__ __forceinline__ explicit SpecGuess(float prior) : a(prior), n(1.f) {}
+  // the tree: acceptance rate bucket / kSpecP
+  __device__ __forceinline__ int bucket() const {
+#ifdef IPMC_SPEC_REJECT_ONLY  // experiments (tools/build_variant.sh): the reject chain only
+    return 0;
 #endif
-    return 2.f * a >= n;
+#if IPMC_SPEC_TREE
+    const int b = (int)((float)kSpecP * a / n + 0.5f);
+    return b < 0 ? 0 : (b > kSpecP ? kSpecP : b);
+#else
+    return 2.f * a >= n ? kSpecP : 0;
+#endif
   }
   __device__ __forceinline__ void settle(int nar, int used) {
 #ifdef IPMC_SPEC_GUESS_CUMULATIVE  // experiments: rounds 1-3's whole-launch ratio
@@ -215,44 +234,80 @@ struct SpecGuess {
   bool fresh = true;
 #endif
 };
-// The prior at a launch's first round: the chain's accept counter over the
-// steps it has counted before the launch (step0 - accepts_step0: a resumed or
-// continued run counts from its own first step, not from global step 0);
-// accept mode without any history.
-__device__ __forceinline__ bool spec_accept_prior(const ipmc_sweep& s, int64_t chain) {
-  if (!s.accepts || s.step0 <= s.accepts_step0) return true;
-  return (uint64_t)(2 * s.accepts[chain]) >= s.step0 - s.accepts_step0;
+// The prior at a launch's first round: the chain's acceptance over the steps
+// it has counted before the launch (step0 - accepts_step0: a resumed or
+// continued run counts from its own first step, not from global step 0); 1
+// without any history.
+__device__ __forceinline__ float spec_accept_prior(const ipmc_sweep& s, int64_t chain) {
+  if (!s.accepts || s.step0 <= s.accepts_step0) return 1.f;
+  return (float)s.accepts[chain] / (float)(s.step0 - s.accepts_step0);
 }
 
 struct SpecRound {
-  int first;  // the first slot whose guess failed (S: none)
   int used;   // steps settled by the round
   int nar;    // accepted steps among them
-  int win;    // the slot whose proposal is the chain's new state (-1: unchanged)
+  int win;    // the node whose proposal is the chain's new state (-1: unchanged)
+  int calls;  // evaluated (in-box) proposals among them
 };
-// From the slots' decisions: slot s's at bit s*L of acc_bits (L lanes per slot).
-__device__ __forceinline__ SpecRound spec_round(bool amode, unsigned long long acc_bits, int S, int L, int64_t left) {
-  const int lim = left < S ? (int)left : S;
-  SpecRound r;
-  if (!amode) {
-    r.first = acc_bits ? __builtin_ctzll(acc_bits) / L : S;
-    r.used = r.first < S ? r.first + 1 : lim;
-    r.nar = r.first < S ? 1 : 0;
-    r.win = r.first < S ? r.first : -1;
-  } else {
-    unsigned long long ev = 0;  // the evaluated slots' bits
-    for (int q = 0; q < lim; ++q) ev |= 1ull << (q * L);
-    const unsigned long long rej = ev & ~acc_bits;
-    r.first = rej ? __builtin_ctzll(rej) / L : S;
-    r.used = r.first < S ? r.first + 1 : lim;
-    r.nar = r.first < S ? r.first : lim;
-    r.win = r.nar - 1;
+// What the walk needs of node n: its decision, whether its proposal was
+// evaluated (ConstrainAccepter) and the next node after a reject / an accept.
+struct SpecStep {
+  bool acc, ok;
+  int next_rej, next_acc;
+};
+// Walk the round's tree from node 0 along the decisions (node(n) -> SpecStep),
+// calling visit(q, la) for every settled step q = 0, 1, ... with la the node
+// whose proposal is the state after step st+q (-1: the round's starting
+// state).  Stops after `left` steps or at a next node outside the S slots.
+template <class Node, class Visit>
+__device__ __forceinline__ SpecRound spec_walk(int S, int64_t left, Node&& node, Visit&& visit) {
+  SpecRound r{0, 0, -1, 0};
+  int n = 0;
+  while (true) {
+    const SpecStep x = node(n);
+    r.calls += x.ok ? 1 : 0;
+    if (x.acc) {
+      ++r.nar;
+      r.win = n;
+    }
+    visit(r.used, r.win);
+    ++r.used;
+    const int c = x.acc ? x.next_acc : x.next_rej;
+    if (r.used >= left || c < 0 || c >= S) break;
+    n = c;
   }
   return r;
 }
-// The slot whose proposal is the chain's state after step st+q of the round (-1: the old state).
-__device__ __forceinline__ int spec_last_acc(const SpecRound& r, bool amode, int q) {
-  return amode ? (q < r.nar ? q : r.nar - 1) : (q == r.first ? r.first : -1);
+// The same path again for the recorded states, as a counted loop over the
+// `used` steps the walk settled (visit(q, la) as in spec_walk).  Kept apart
+// from spec_walk: a cross-lane read of the proposals inside the walk's
+// data-dependent loop gave wrong states in the Burgers kernel with two chains
+// per wave (tools/probes/spec_tree_debug.py), the counted loop and LDS reads
+// do not.
+template <class Node, class Visit>
+__device__ __forceinline__ void spec_replay(int used, Node&& node, Visit&& visit) {
+  int n = 0, la = -1;
+  for (int q = 0; q < used; ++q) {
+    const SpecStep x = node(n);
+    if (x.acc) la = n;
+    visit(q, la);
+    n = x.acc ? x.next_acc : x.next_rej;
+  }
+}
+// Node n's step from the slots' decision bits (bit n*L of acc / ok, L lanes
+// per slot) and the tree table.
+__device__ __forceinline__ SpecStep spec_step_bits(const SpecNode* tree, int n, int L, unsigned long long acc,
+                                                   unsigned long long ok) {
+  const SpecNode& x = tree[n];
+  return SpecStep{((acc >> (n * L)) & 1ull) != 0, ((ok >> (n * L)) & 1ull) != 0, x.child[0], x.child[1]};
+}
+__device__ __forceinline__ int spec_pack_children(const SpecNode& x) {
+  return (int)(uint16_t)x.child[0] | ((int)x.child[1] << 16);
+}
+__device__ __forceinline__ SpecStep spec_step_packed(int packed, int n, int L, unsigned long long acc,
+                                                     unsigned long long ok) {
+  return SpecStep{((acc >> (n * L)) & 1ull) != 0, ((ok >> (n * L)) & 1ull) != 0,
+                  (int)(int16_t)(packed & 0xFFFF), packed >> 16};
 }
 
 // Running sums Σu, Σu² (ipmc_sweep.sum_u / sum_u2) of a lane's n <= N

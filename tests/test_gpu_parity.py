@@ -731,11 +731,11 @@ def test_burgers_every_layout_bit_exact(dev, orc, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
-    """small_spec_kernel (S lanes evaluate S consecutive steps; along the reject
-    path the first acceptance ends the round, along the accept path the first
-    rejection) equals the sequential chain bit for bit, for every width, with
-    schedules, box constraint, sums and the RW regularizer, at low and high
-    acceptance."""
+    """small_spec_kernel (S lanes = the first S nodes of the speculation tree
+    for the chain's recent acceptance rate: the reject chain, the accept chain
+    or a branching tree between them) equals the sequential chain bit for bit,
+    for every width, with schedules, box constraint, sums and the RW
+    regularizer, at low, intermediate and high acceptance."""
     from ip_mcmc_amd import LinearOperator, Lorenz63Operator
 
     rng = np.random.default_rng(23)
@@ -774,7 +774,7 @@ def test_small_speculative_sweeps_bit_exact(dev, orc, dtype):
             d = _sweep_device(op, U0, phr, y, ginv, sq, 0.2, 9, 0, n, dtype, dev, spec=w, proposal="rw",
                               reg_scale=rs)
             _assert_same(d, o, (type(op).__name__, "rw", w))
-    assert high >= 10, high  # the accept-mode path ran
+    assert high >= 10, high  # the accept-chain trees ran
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
@@ -818,7 +818,10 @@ def test_l96_speculative_sweeps_bit_exact(dev, orc, dtype):
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
     """Speculative slots in the two-scale (S·K lanes per chain) and Burgers
-    (S·GS lanes) sweeps equal the sequential chain bit for bit."""
+    (S·GS lanes) sweeps equal the sequential chain bit for bit, at 10-45 %
+    acceptance (branching trees) and 80-97 % (the accept chain), with sums --
+    the Burgers cases with two chains per wave caught the recorded-state bug
+    spec_replay avoids (ipmc_sweep_common.hpp)."""
     from ip_mcmc_amd import BurgersOperator, TwoScaleLorenz96Operator
 
     n = 17
@@ -835,8 +838,8 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
     high = 0
     for (op, widths), scale in [(c, sc) for c in cases for sc in (0.2, 3.0)]:
         U0, phi0, y, ginv, sq = _problem(op, 19, dtype, orc, seed=3)
-        # 3.0: 10-45 % of the steps accepted (the two-scale kernel speculates along
-        # the reject path); 0.2: broad enough that 80-97 % are (the accept path)
+        # 3.0: 10-45 % of the steps accepted (branching speculation trees); 0.2:
+        # broad enough that 80-97 % are (the accept chain)
         ginv = ginv * scale
         phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
         for kw in (dict(), dict(box=(np.full(3, -0.3), None, None), sched=sched), dict(want_sums=True)):
@@ -855,7 +858,7 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
         d = _sweep_device(op, U0, phr, y, ginv, sq, 0.1, 9, 0, n, dtype, dev, spec=widths[-1], proposal="rw",
                           reg_scale=rs)
         _assert_same(d, o, (type(op).__name__, "rw"))
-    assert high >= 3, high  # the two-scale accept-path rounds ran
+    assert high >= 3, high  # the two-scale accept-chain rounds ran
 
 
 # ------------------------------------------------ non-diagonal priors (L·ξ)

@@ -128,5 +128,27 @@ case "$1" in
     done &&
     timeout -k 10 300 python tools/config_bench.py l96mx1~1@256 l96mx64~1@256 l96mx1024~1@256 >> $O/spec_mixing_nospec.jsonl
     ;;
+  s6)
+    # speculation trees: the speculative parity tests first (stop on a
+    # failure), then the whole suite, then the small-ensemble rows on the
+    # mixing posterior and the accept-nothing problem, config 2 and the
+    # sequential Burgers / two-scale sweeps against the two-path build
+    V=ip_mcmc_amd/lib/variants/pathspec/libipmc.so
+    timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+        -k "speculative or dense_prior or small_models" > $O/pytest_tree_spec.log 2>&1 &&
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_s6.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; } &&
+    R="l96mx1@256 l96mx64@256 l96mx1024@256 l96x1@256 l96x64@256" &&
+    timeout -k 10 300 python tools/config_bench.py $R >> $O/spec_tree_ab.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 300 python tools/config_bench.py $R >> $O/spec_tree_ab.jsonl &&
+    timeout -k 10 300 python tools/config_bench.py cfg2@16384 cfg4 ts6 >> $O/spec_tree_seq_ab.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 300 python tools/config_bench.py cfg2@16384 cfg4 ts6 >> $O/spec_tree_seq_ab.jsonl
+    ;;
+  dbg)
+    timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
+    IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
+        > $O/spec_tree_debug_shfl.txt 2>&1
+    ;;
   *) echo "unknown session $1"; exit 2 ;;
 esac
