@@ -24,18 +24,30 @@
 // expectation against the better chain's 4.2; at p = 0.88, S = 16 it is the
 // accept chain (7.3).
 //
-// The tables are built at compile time: kSpecBuckets acceptance rates p = b /
-// kSpecP, kSpecNodes nodes each, ties broken by creation order (the reject
-// child first).
+// The tables are built at compile time: kSpecBuckets acceptance rates
+// (kSpecGridP: sixteenths, and finer towards 0 and 1, where wide rounds tell
+// 1/32 from 1/16), kSpecNodes nodes each, ties broken by creation order (the
+// reject child first).
 #pragma once
 
 #include <stdint.h>
 
 namespace ipmc {
 
-constexpr int kSpecP = 16;
-constexpr int kSpecBuckets = kSpecP + 1;
+constexpr int kSpecBuckets = 23;
 constexpr int kSpecNodes = 256;
+constexpr double kSpecGridP[kSpecBuckets] = {
+    0.0,         1.0 / 128,   1.0 / 64,    1.0 / 32,    1.0 / 16,     2.0 / 16,   3.0 / 16,   4.0 / 16,
+    5.0 / 16,    6.0 / 16,    7.0 / 16,    8.0 / 16,    9.0 / 16,     10.0 / 16,  11.0 / 16,  12.0 / 16,
+    13.0 / 16,   14.0 / 16,   15.0 / 16,   31.0 / 32,   63.0 / 64,    127.0 / 128, 1.0};
+
+// The bucket nearest an estimated acceptance rate (the midpoints between
+// grid points as thresholds).
+inline constexpr int spec_bucket_of(double p) {
+  int b = 0;
+  for (int i = 0; i + 1 < kSpecBuckets; ++i) b += p > 0.5 * (kSpecGridP[i] + kSpecGridP[i + 1]) ? 1 : 0;
+  return b;
+}
 
 struct SpecNode {
   int16_t orig;  // the node whose proposal this one starts from (-1: the round's state)
@@ -93,7 +105,7 @@ struct Heap {
 constexpr SpecTrees make_spec_trees() {
   SpecTrees t{};
   for (int b = 0; b < kSpecBuckets; ++b) {
-    const double p = (double)b / kSpecP;
+    const double p = kSpecGridP[b];
     spec_tree_detail::Heap heap{};
     int seq = 0;
     heap.push({1.0, seq++, -1, 0});

@@ -198,25 +198,29 @@ static __constant__ const SpecTrees kSpecTrees = make_spec_trees();
 #ifndef IPMC_SPEC_TREE  // 0: rounds 3-4's two paths only, reject or accept chain (A/B)
 #define IPMC_SPEC_TREE 1
 #endif
+#ifndef IPMC_SPEC_MEMORY  // the acceptance estimate's weight per round back (A/B)
+#define IPMC_SPEC_MEMORY 0.75f
+#endif
 
 // The chain's recent acceptance rate: accepted and settled steps summed over
-// its rounds with weight 3/4 per round back (~4 rounds).  Rounds 1-3 used the
-// whole launch's ratio, which lags behind a posterior whose acceptance changes
-// along the run (burn-in, a step-size schedule) once launches are long
+// its rounds with weight 3/4 per round back (~4 rounds).  A chain's accepts
+// come in bursts (a chain leaving a local minimum accepts several steps in a
+// row), which a short memory follows; rounds 1-3 used the whole launch's
+// ratio, which also lags behind a posterior whose acceptance changes along
+// the run (burn-in, a step-size schedule) once launches are long
 // (sampler.STEPS_PER_LAUNCH).  Before its first round: `prior`.
 struct SpecGuess {
   float a, n;  // recency-weighted accepted / settled steps
   __device__ __forceinline__ explicit SpecGuess(float prior) : a(prior), n(1.f) {}
-  // the tree: acceptance rate bucket / kSpecP
+  // the tree: the grid bucket nearest the estimated acceptance rate
   __device__ __forceinline__ int bucket() const {
 #ifdef IPMC_SPEC_REJECT_ONLY  // experiments (tools/build_variant.sh): the reject chain only
     return 0;
 #endif
 #if IPMC_SPEC_TREE
-    const int b = (int)((float)kSpecP * a / n + 0.5f);
-    return b < 0 ? 0 : (b > kSpecP ? kSpecP : b);
+    return spec_bucket_of((double)(a / n));
 #else
-    return 2.f * a >= n ? kSpecP : 0;
+    return 2.f * a >= n ? kSpecBuckets - 1 : 0;
 #endif
   }
   __device__ __forceinline__ void settle(int nar, int used) {
@@ -226,8 +230,8 @@ struct SpecGuess {
     a += (float)nar;
     n += (float)used;
 #else
-    a = fmaf(0.75f, a, (float)nar);
-    n = fmaf(0.75f, n, (float)used);
+    a = fmaf(IPMC_SPEC_MEMORY, a, (float)nar);
+    n = fmaf(IPMC_SPEC_MEMORY, n, (float)used);
 #endif
   }
 #ifdef IPMC_SPEC_GUESS_CUMULATIVE

@@ -861,6 +861,37 @@ def test_ts_and_burgers_speculative_sweeps_bit_exact(dev, orc, dtype):
     assert high >= 3, high  # the two-scale accept-chain rounds ran
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_speculative_recorded_states_short_launches(dev, orc, dtype):
+    """Running sums of speculative sweeps at launch lengths 1, 2, 3 and 5 (a
+    round cut short by the launch's end, trees of every shape at 10-97 %
+    acceptance), every kernel family, with several chains per wave: the
+    recorded states are the ones the walk settled (spec_replay) -- the case
+    that caught cross-lane reads inside the walk (Burgers, two chains per
+    wave).  In-launch samples: tests/test_gpu_run.py."""
+    from ip_mcmc_amd import BurgersOperator, Lorenz63Operator, Lorenz96Operator, TwoScaleLorenz96Operator
+
+    rng = np.random.default_rng(12)
+    cases = [(BurgersOperator(N=128, dt_mode="cfl", T=0.2), (2, 4, 16)),
+             (TwoScaleLorenz96Operator(K=6, J=4, x0=rng.normal(size=30), dt=0.004, n_steps=25), (2, 4, 8)),
+             (Lorenz96Operator(8, 8.0, dt=0.005, n_steps=40), (2, 8, 0)),
+             (Lorenz63Operator(x0=(1.0, 2.0, 20.0), dt=0.01, n_steps=100), (2, 8, 64))]
+    for op, widths in cases:
+        for scale in (0.2, 3.0):
+            U0, phi0, y, ginv, sq = _problem(op, 19, dtype, orc, seed=3)
+            ginv = ginv * scale
+            phi0 = orc.potential(op, U0, y, ginv, _np(dtype)).astype(np.float64)
+            for n in (1, 2, 3, 5):
+                o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.3, 8, 2**32 - 3, n, dtype, want_sums=True)
+                for w in widths:
+                    d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.3, 8, 2**32 - 3, n, dtype, dev, spec=w,
+                                      want_sums=True)
+                    what = (type(op).__name__, scale, n, w)
+                    _assert_same(d, o, what)
+                    assert np.array_equal(d["sum_u"], o["sum_u"]), what
+                    assert np.array_equal(d["sum_u2"], o["sum_u2"]), what
+
+
 # ------------------------------------------------ non-diagonal priors (L·ξ)
 def _dense_chol(k, seed):
     """A random SPD prior covariance's lower Cholesky factor (correlated components)."""

@@ -24,7 +24,11 @@ PROG = r"""
 using namespace ipmc;
 static const SpecTrees T = make_spec_trees();
 int main() {
-  std::printf("{\"P\": %%d, \"nodes\": %%d, \"trees\": [", kSpecP, kSpecNodes);
+  std::printf("{\"nodes\": %%d, \"p\": [", kSpecNodes);
+  for (int b = 0; b < kSpecBuckets; ++b) std::printf("%%s%%.17g", b ? "," : "", kSpecGridP[b]);
+  std::printf("], \"bucket_of\": [");
+  for (int i = 0; i <= 1000; ++i) std::printf("%%s%%d", i ? "," : "", spec_bucket_of(i / 1000.0));
+  std::printf("], \"trees\": [");
   for (int b = 0; b < kSpecBuckets; ++b) {
     std::printf("%%s[", b ? "," : "");
     for (int i = 0; i < kSpecNodes; ++i) {
@@ -62,10 +66,10 @@ def _paths(tree):
 
 
 def test_trees_are_consistent_best_first_prefixes(tables):
-    P, N = tables["P"], tables["nodes"]
-    assert len(tables["trees"]) == P + 1
+    N, grid = tables["nodes"], tables["p"]
+    assert len(tables["trees"]) == len(grid) and grid[0] == 0 and grid[-1] == 1
     for b, tree in enumerate(tables["trees"]):
-        p = b / P
+        p = grid[b]
         assert len(tree) == N
         path, parent = _paths(tree)
         assert sorted(path) == list(range(N))  # every node reachable from the root
@@ -90,7 +94,7 @@ def test_trees_are_consistent_best_first_prefixes(tables):
         assert all(prob[i] >= prob[i + 1] - 1e-15 for i in range(N - 1)), b
         if b == 0:
             assert all(t[2] == -1 and t[0] == -1 and t[3] == i for i, t in enumerate(tree))  # the reject chain
-        if b == P:
+        if b == len(grid) - 1:
             assert all(t[1] == -1 and t[0] == i - 1 and t[3] == i for i, t in enumerate(tree))  # the accept chain
 
 
@@ -107,9 +111,9 @@ def test_trees_are_optimal(tables):
     """No tree of S nodes settles more steps in expectation: the optimum by
     dynamic programming over the sizes of the reject and accept subtrees,
     V(S) = 1 + max_a [(1-p) V(a) + p V(S-1-a)]."""
-    P = tables["P"]
-    for b in (1, 4, 8, 12, 15):
-        p = b / P
+    grid = tables["p"]
+    for b in (1, 3, 5, 8, 11, 15, 18, 21):
+        p = grid[b]
         V = [0.0]
         for S in range(1, 65):
             V.append(1 + max((1 - p) * V[a] + p * V[S - 1 - a] for a in range(S)))
@@ -121,11 +125,20 @@ def test_speculation_gain_over_the_chains(tables):
     """The numbers DESIGN quotes: a mixing chain (p = 0.25) settles 7.25 steps
     per 64-slot round with the tree against 4.0 along the reject chain; at p =
     0.875 and 16 slots the tree is the accept chain."""
-    t4 = tables["trees"][4]
+    grid = tables["p"]
+    t4 = tables["trees"][grid.index(0.25)]
     assert _expected_steps(t4, 64, 0.25) == pytest.approx(7.25, abs=0.01)
     assert sum(0.75**i for i in range(64)) == pytest.approx(4.0, abs=0.01)
-    t14 = tables["trees"][14]
+    t14 = tables["trees"][grid.index(0.875)]
     assert [t[3] for t in t14[:16]] == list(range(16))
+
+
+def test_bucket_is_the_nearest_grid_rate(tables):
+    grid = np.array(tables["p"])
+    for i, b in enumerate(tables["bucket_of"]):
+        p = i / 1000
+        d = np.abs(grid - p)
+        assert d[b] == d.min(), (p, b)
 
 
 def test_walk_replays_the_sequential_chain(tables):
@@ -134,9 +147,8 @@ def test_walk_replays_the_sequential_chain(tables):
     origin = the last accepted visited node), and the walk stops at the first
     node whose next node is outside the S slots (or after `left` steps)."""
     rng = np.random.default_rng(5)
-    P = tables["P"]
     for _ in range(400):
-        b = int(rng.integers(0, P + 1))
+        b = int(rng.integers(0, len(tables["p"])))
         S = int(rng.choice([1, 2, 4, 8, 16, 32, 64, 256]))
         left = int(rng.integers(1, 80))
         tree = tables["trees"][b]

@@ -145,6 +145,80 @@ case "$1" in
     timeout -k 10 300 python tools/config_bench.py cfg2@16384 cfg4 ts6 >> $O/spec_tree_seq_ab.jsonl &&
     IPMC_LIB_PATH=$V timeout -k 10 300 python tools/config_bench.py cfg2@16384 cfg4 ts6 >> $O/spec_tree_seq_ab.jsonl
     ;;
+  s7)
+    # the reference's studies (examples/) with speculation trees against the
+    # two-path build, 1 024 chains and one chain; the sequential Burgers /
+    # two-scale sweeps again, interleaved
+    V=ip_mcmc_amd/lib/variants/pathspec/libipmc.so
+    for lib in "" "$V"; do
+      tag=${lib:+pathspec}; tag=${tag:-tree}
+      for args in "burgers_beta.py 1024" "burgers_beta.py 1" "lorenz_thesis.py 1024" "lorenz_thesis.py 1" "lorenz63_config2.py"; do
+        set -- $args
+        IPMC_LIB_PATH=$lib timeout -k 10 300 python examples/$1 ${2:-} > $O/ex_tmp.jsonl || exit 1
+        python -c "import json,sys;[print(json.dumps(dict(json.loads(l),build='$tag',example='$1',arg='${2:-}'))) for l in open('$O/ex_tmp.jsonl') if l.startswith('{')]" >> $O/examples_tree_ab.jsonl || exit 1
+      done
+    done &&
+    for i in 1 2; do
+      timeout -k 10 300 python tools/config_bench.py cfg4 ts6 >> $O/seq_tree_ab2.jsonl &&
+      IPMC_LIB_PATH=$V timeout -k 10 300 python tools/config_bench.py cfg4 ts6 >> $O/seq_tree_ab2.jsonl || exit 1
+    done
+    ;;
+  s8)
+    # speculation trees with the finer rate grid and 0.95 memory: speculative
+    # parity tests, the small-ensemble rows and the studies against the
+    # two-path build, then the whole suite
+    V=ip_mcmc_amd/lib/variants/pathspec/libipmc.so
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+        -k "speculative or dense_prior or small_models" > $O/pytest_tree_spec2.log 2>&1 &&
+    R="l96mx1@256 l96mx64@256 l96mx1024@256 l96x1@256 l96x64@256" &&
+    timeout -k 10 300 python tools/config_bench.py $R cfg2@16384 >> $O/spec_tree_ab2.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 300 python tools/config_bench.py $R cfg2@16384 >> $O/spec_tree_ab2.jsonl &&
+    for lib in "" "$V"; do
+      tag=${lib:+pathspec}; tag=${tag:-tree}
+      for args in "burgers_beta.py 1024" "burgers_beta.py 1" "lorenz_thesis.py 1024" "lorenz_thesis.py 1"; do
+        set -- $args
+        IPMC_LIB_PATH=$lib timeout -k 10 300 python examples/$1 ${2:-} > $O/ex_tmp.jsonl || exit 1
+        python -c "import json,sys;[print(json.dumps(dict(json.loads(l),build='$tag',example='$1',arg='${2:-}'))) for l in open('$O/ex_tmp.jsonl') if l.startswith('{')]" >> $O/examples_tree_ab2.jsonl || exit 1
+      done
+    done &&
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_s8.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; }
+    ;;
+  s9)
+    # Burgers small ensembles: trees vs two paths vs no speculation, CFL and fixed step
+    V=ip_mcmc_amd/lib/variants/pathspec/libipmc.so
+    P="python tools/probes/burgers_spec_probe.py"
+    for i in 1 2; do
+      timeout -k 10 200 $P 1024 >> $O/burgers_spec_probe.jsonl &&
+      IPMC_LIB_PATH=$V timeout -k 10 200 $P 1024 >> $O/burgers_spec_probe.jsonl || exit 1
+    done &&
+    timeout -k 10 200 $P 1024 1 >> $O/burgers_spec_probe.jsonl &&
+    timeout -k 10 200 $P 1 >> $O/burgers_spec_probe.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 200 $P 1 >> $O/burgers_spec_probe.jsonl
+    ;;
+  s10)
+    # estimator memory 3/4 (product) vs 0.95 vs the two paths: Burgers
+    # studies (CFL and fixed step), the mixing rows, the Lorenz study
+    P="python tools/probes/burgers_spec_probe.py"
+    R="l96mx1@256 l96mx64@256 l96mx1024@256 cfg2@16384"
+    for lib in "" ip_mcmc_amd/lib/variants/m095/libipmc.so ip_mcmc_amd/lib/variants/pathspec/libipmc.so; do
+      IPMC_LIB_PATH=$lib timeout -k 10 200 $P 1024 >> $O/mem_ab_burgers.jsonl &&
+      IPMC_LIB_PATH=$lib timeout -k 10 200 $P 1 >> $O/mem_ab_burgers.jsonl &&
+      IPMC_LIB_PATH=$lib timeout -k 10 200 python tools/config_bench.py $R | \
+        python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin]" >> $O/mem_ab_rows.jsonl &&
+      IPMC_LIB_PATH=$lib timeout -k 10 200 python examples/lorenz_thesis.py 1024 | \
+        python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin if l.startswith('{')]" >> $O/mem_ab_lorenz.jsonl || exit 1
+    done
+    ;;
+  s11)
+    # run-to-run spread of the Burgers pCN CFL study (1 024 chains), three builds interleaved
+    P="python tools/probes/burgers_spec_probe.py"
+    for i in 1 2 3; do
+      for lib in "" ip_mcmc_amd/lib/variants/m095/libipmc.so ip_mcmc_amd/lib/variants/pathspec/libipmc.so; do
+        IPMC_LIB_PATH=$lib timeout -k 10 200 $P 1024 0 pcn-cfl >> $O/burgers_pcn_cfl_spread.jsonl || exit 1
+      done
+    done
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
