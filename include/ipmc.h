@@ -176,7 +176,7 @@ typedef struct ipmc_sweep {
                                  sample_step_stride >= (n_chains-1)*sample_stride + k ([sample, chain, k]) */
   uint64_t accepts_step0;   /* (ABI 11) global pCN step at which the `accepts` counters started counting
                                (MCMCSampler.run zeroes them at its first step; 0 = from step 0).  A speculative
-                               sweep's first round guesses accept mode when a chain accepted at least half of its
+                               sweep's first round picks its speculation tree by the chain's acceptance over the
                                steps since then (step0 - accepts_step0); results never depend on it. */
 } ipmc_sweep;
 

@@ -219,6 +219,21 @@ case "$1" in
       done
     done
     ;;
+  final)
+    # the final tree: the whole suite, the published line with its same-box
+    # profiles, the small-ensemble rows and the reference studies
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_final.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; } &&
+    bash tools/sessions/r4.sh s2prof &&
+    timeout -k 10 300 python tools/config_bench.py l96mx1@256 l96mx64@256 l96mx1024@256 l96x1@256 l96x64@256 \
+        cfg2@16384 > $O/spec_final.jsonl &&
+    for args in "burgers_beta.py 1024" "burgers_beta.py 1" "lorenz_thesis.py 1024" "lorenz_thesis.py 1" \
+                "lorenz63_config2.py" "stuart_reference.py"; do
+      set -- $args
+      timeout -k 10 300 python examples/$1 ${2:-} > $O/ex_tmp.jsonl || exit 1
+      python -c "import json,sys;[print(json.dumps(dict(json.loads(l),example='$1',arg='${2:-}'))) for l in open('$O/ex_tmp.jsonl') if l.startswith('{')]" >> $O/examples_final.jsonl || exit 1
+    done
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
