@@ -234,6 +234,22 @@ case "$1" in
       python -c "import json,sys;[print(json.dumps(dict(json.loads(l),example='$1',arg='${2:-}'))) for l in open('$O/ex_tmp.jsonl') if l.startswith('{')]" >> $O/examples_final.jsonl || exit 1
     done
     ;;
+  s12b)
+    # kernel trace of the Burgers pCN CFL study, 1 024 chains, auto speculation and none
+    for sp in 0 1; do
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/burtrace$sp -o run -- \
+          python tools/probes/burgers_spec_probe.py 1024 $sp pcn-cfl > $O/burtrace$sp.json || exit 1
+    done
+    ;;
+  s13)
+    # Burgers studies at 1 024 and 256 chains: speculation width 1 / 2 / 4 / auto, CFL and fixed step
+    P="python tools/probes/burgers_spec_probe.py"
+    for sp in 1 2 4 0; do
+      timeout -k 10 200 $P 1024 $sp >> $O/burgers_width_scan.jsonl || exit 1
+    done &&
+    timeout -k 10 200 $P 256 1 >> $O/burgers_width_scan.jsonl &&
+    timeout -k 10 200 $P 256 0 >> $O/burgers_width_scan.jsonl
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
