@@ -1,6 +1,14 @@
 #!/bin/bash
 # Round-4 GPU sessions: bash tools/sessions/r4.sh <name>
 # Every GPU step has its own time limit and the steps are chained with &&.
+# The A/B sessions load variant builds of libipmc.so (not kept in the tree;
+# rebuild them on the CPU first):
+#   l63scalar  tools/build_variant.sh l63scalar ipmc_api.hip -DIPMC_L63_PK=0
+#   speck8     tools/build_variant.sh speck8 ipmc_api.hip -DIPMC_SPEC_K3=0
+#   pathspec   make -C ip_mcmc_amd/csrc -j8 OBJDIR=../../build/variants/pathspec \
+#                OUT=../lib/variants/pathspec/libipmc.so \
+#                HOST_OUT=../../build/variants/pathspec/libipmc_host.so EXTRA=-DIPMC_SPEC_TREE=0
+#   m095       the same with m095 and EXTRA=-DIPMC_SPEC_MEMORY=0.95f
 set -o pipefail
 cd "$(dirname "$0")/../.."
 O=gpurun_out/r4
