@@ -60,6 +60,15 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
   }
 }
 
+// experiments: RK4 steps per loop iteration (-DIPMC_L96_UNROLL=2); default: the compiler's choice
+#if defined(IPMC_L96_UNROLL) && IPMC_L96_UNROLL > 0
+#define IPMC_L96_STR_(x) #x
+#define IPMC_L96_UNROLL_PRAGMA(n) _Pragma(IPMC_L96_STR_(unroll n))
+#define IPMC_L96_RK_UNROLL IPMC_L96_UNROLL_PRAGMA(IPMC_L96_UNROLL)
+#else
+#define IPMC_L96_RK_UNROLL
+#endif
+
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
 // V is the per-lane storage type (float, double, or f32x2 = two fp32 chains),
 // S the scalar type of the problem constants, IL: interleaved groups of 8
@@ -77,6 +86,7 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     x[j] = P::of(x0[j]);
     ob[j] = P::of((S)0);
   }
+  IPMC_L96_RK_UNROLL
   for (int n = 0; n < nsteps; ++n) {
     V acc[M], xs[M];
     l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);

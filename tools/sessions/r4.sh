@@ -258,6 +258,43 @@ case "$1" in
     timeout -k 10 200 $P 256 1 >> $O/burgers_width_scan.jsonl &&
     timeout -k 10 200 $P 256 0 >> $O/burgers_width_scan.jsonl
     ;;
+  s14)
+    # config 2: the Lorenz-63 RK4 loop unrolled by 2 and 4 against the compiler's choice, interleaved
+    for i in 1 2; do
+      for lib in "" ip_mcmc_amd/lib/variants/l63u2/libipmc.so ip_mcmc_amd/lib/variants/l63u4/libipmc.so; do
+        IPMC_LIB_PATH=$lib timeout -k 10 200 python tools/config_bench.py cfg2@16384 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin]" >> $O/l63_unroll_ab.jsonl || exit 1
+      done
+    done
+    ;;
+  s15)
+    # the Lorenz-63 RK loop unrolled by 4 (product): its parity tests, the
+    # unroll A/B (compiler's choice / 4 / 8), the config-2 study, the whole suite
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests \
+        -m gpu -k "small or cfg2 or l63 or L63 or dense_prior or speculative" > $O/pytest_l63_unroll.log 2>&1 &&
+    for i in 1 2; do
+      for lib in ip_mcmc_amd/lib/variants/l63u0/libipmc.so "" ip_mcmc_amd/lib/variants/l63u8/libipmc.so; do
+        IPMC_LIB_PATH=$lib timeout -k 10 200 python tools/config_bench.py cfg2@16384 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product_u4}'))) for l in sys.stdin]" >> $O/l63_unroll_ab2.jsonl || exit 1
+      done
+    done &&
+    timeout -k 10 200 python examples/lorenz63_config2.py > $O/example_l63_cfg2.jsonl &&
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_s15.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -le 1 ]; }
+    ;;
+  s16)
+    # the Lorenz-96 RK loop unrolled by 2 (variant) against the product: the
+    # headline kernel leg and the small-ensemble rows, interleaved
+    V=ip_mcmc_amd/lib/variants/l96u2/libipmc.so
+    for i in 1 2; do
+      for lib in "" "$V"; do
+        IPMC_LIB_PATH=$lib timeout -k 10 300 python bench.py --kernel-only --no-cpu --steps 50 --warmup 5 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin if l.startswith('{')]" >> $O/l96_unroll_ab.jsonl &&
+        IPMC_LIB_PATH=$lib timeout -k 10 300 python tools/config_bench.py l96mx1@256 l96mx64@256 l96mx1024@256 l96x64@256 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin]" >> $O/l96_unroll_ab.jsonl || exit 1
+      done
+    done
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
