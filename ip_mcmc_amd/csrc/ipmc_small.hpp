@@ -31,7 +31,7 @@ __device__ __forceinline__ void l63_rhs(T sg, T rh, T bb, const T (&s)[3], T (&o
 // 455 -> 501 M steps/s in f64, 549 -> 604 M in fp32 against the compiler's
 // own choice (profiles/r4/l63_unroll_ab.jsonl).  0: the compiler's choice.
 #ifndef IPMC_L63_UNROLL
-#define IPMC_L63_UNROLL 4
+#define IPMC_L63_UNROLL 8
 #endif
 #if IPMC_L63_UNROLL > 0
 #define IPMC_STR_(x) #x
@@ -538,20 +538,16 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
     if (ok) acc = (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
     const unsigned long long accm = (__ballot(acc) >> gbase) & gmask;
     const unsigned long long okm = (__ballot(ok) >> gbase) & gmask;
-    const int kids = spec_pack_children(nd);
-    const SpecRound rd = spec_walk(
-        S, left,
-        [&](int n) { return spec_step_packed(__shfl(kids, gbase + n, 64), n, 1, accm, okm); },
-        [](int, int) {});
+    // the walk resolved in parallel: each lane tests whether its node is on the path
+    const unsigned long long path = (__ballot(spec_on_path(tb, sub, accm, act)) >> gbase) & gmask;
+    const SpecRound rd = spec_path_round(path, accm, okm);
     const T phf = __shfl(phv, gbase + (rd.win >= 0 ? rd.win : 0), 64);
     if (sub == 0 && (s.sum_u || (s.sample_every > 0 && clk.next < st + rd.used))) {
       // the states after each settled step, in step order: the same walk again
       const bool sums = s.sum_u != nullptr;
       RoundSums<KM> rsum(sums ? s.sum_u + chain * k : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * k : nullptr,
                          sums ? k : 0);
-      const SpecNode* tree = kSpecTrees.nd[tb];
-      spec_replay(rd.used, [&](int n) { return spec_step_bits(tree, n, 1, accm, okm); },
-                  [&](int q, int la) {
+      spec_path_replay(path, accm, [&](int q, int la) {
                   if (sums) {
 #pragma unroll
                     for (int j = 0; j < KM; ++j)

@@ -56,9 +56,16 @@ struct SpecNode {
   uint8_t lvl;    // accepted edges on the path: proposals formed before this one
 };
 
+// In-wave rounds (at most 64 slots) resolve the walk in parallel: node n is
+// on the realized path iff every ancestor a decided the way n's path goes
+// there -- ((acc ^ edge[n]) & anc[n]) == 0 over the slots' decision bits.
+constexpr int kSpecWaveNodes = 64;
+
 struct SpecTrees {
   SpecNode nd[kSpecBuckets][kSpecNodes];
   uint8_t maxlvl[kSpecBuckets][kSpecNodes + 1];  // max lvl over the first n nodes
+  uint64_t anc[kSpecBuckets][kSpecWaveNodes];    // node n's ancestors (bit a)
+  uint64_t edge[kSpecBuckets][kSpecWaveNodes];   // ... and the decision its path takes at each (1: accept)
 };
 
 namespace spec_tree_detail {
@@ -128,6 +135,14 @@ constexpr SpecTrees make_spec_trees() {
       }
       ml = x.lvl > ml ? x.lvl : ml;
       t.maxlvl[b][i + 1] = (uint8_t)ml;
+      if (i < kSpecWaveNodes) {
+        t.anc[b][i] = 0;
+        t.edge[b][i] = 0;
+        if (c.parent >= 0) {  // the parent's ancestors plus the parent itself
+          t.anc[b][i] = t.anc[b][c.parent] | (uint64_t(1) << c.parent);
+          t.edge[b][i] = t.edge[b][c.parent] | (uint64_t(c.edge) << c.parent);
+        }
+      }
       heap.push({c.pr * (1.0 - p), seq++, i, 0});
       heap.push({c.pr * p, seq++, i, 1});
     }

@@ -218,7 +218,11 @@ struct SpecGuess {
     return 0;
 #endif
 #if IPMC_SPEC_TREE
-    return spec_bucket_of((double)(a / n));
+    const float p = a / n;  // the grid's midpoints in fp32 (any tree is correct; this only picks one)
+    int b = 0;
+#pragma unroll
+    for (int i = 0; i + 1 < kSpecBuckets; ++i) b += p > (float)(0.5 * (kSpecGridP[i] + kSpecGridP[i + 1])) ? 1 : 0;
+    return b;
 #else
     return 2.f * a >= n ? kSpecBuckets - 1 : 0;
 #endif
@@ -298,6 +302,36 @@ __device__ __forceinline__ void spec_replay(int used, Node&& node, Visit&& visit
     n = x.acc ? x.next_acc : x.next_rej;
   }
 }
+// In-wave rounds (S <= 64 slots, one decision bit per slot): the walk
+// resolved in parallel.  Every lane computes whether its own node lies on the
+// realized path (spec_on_path), a ballot gathers the path, and the path's
+// nodes in index order are its steps in order (a child's index exceeds its
+// parent's).  `path`, `acc`, `ok` hold one bit per slot (bit n = node n).
+__device__ __forceinline__ bool spec_on_path(int tb, int node, unsigned long long acc, bool act) {
+  return act && ((acc ^ kSpecTrees.edge[tb][node]) & kSpecTrees.anc[tb][node]) == 0;
+}
+__device__ __forceinline__ SpecRound spec_path_round(unsigned long long path, unsigned long long acc,
+                                                     unsigned long long ok) {
+  SpecRound r;
+  r.used = __builtin_popcountll(path);
+  r.nar = __builtin_popcountll(path & acc);
+  r.calls = __builtin_popcountll(path & ok);
+  const unsigned long long pa = path & acc;
+  r.win = pa ? 63 - __builtin_clzll(pa) : -1;  // the deepest accepted node of the path
+  return r;
+}
+// visit(q, la) over the path's steps, as spec_walk's
+template <class Visit>
+__device__ __forceinline__ void spec_path_replay(unsigned long long path, unsigned long long acc, Visit&& visit) {
+  int la = -1, q = 0;
+  while (path) {
+    const int n = __builtin_ctzll(path);
+    path &= path - 1;
+    if ((acc >> n) & 1ull) la = n;
+    visit(q++, la);
+  }
+}
+
 // Node n's step from the slots' decision bits (bit n*L of acc / ok, L lanes
 // per slot) and the tree table.
 __device__ __forceinline__ SpecStep spec_step_bits(const SpecNode* tree, int n, int L, unsigned long long acc,

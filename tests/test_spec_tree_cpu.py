@@ -28,6 +28,14 @@ int main() {
   for (int b = 0; b < kSpecBuckets; ++b) std::printf("%%s%%.17g", b ? "," : "", kSpecGridP[b]);
   std::printf("], \"bucket_of\": [");
   for (int i = 0; i <= 1000; ++i) std::printf("%%s%%d", i ? "," : "", spec_bucket_of(i / 1000.0));
+  std::printf("], \"anc\": [");
+  for (int b = 0; b < kSpecBuckets; ++b) {
+    std::printf("%%s[", b ? "," : "");
+    for (int i = 0; i < kSpecWaveNodes; ++i)
+      std::printf("%%s[\"%%llu\",\"%%llu\"]", i ? "," : "", (unsigned long long)T.anc[b][i],
+                  (unsigned long long)T.edge[b][i]);
+    std::printf("]");
+  }
   std::printf("], \"trees\": [");
   for (int b = 0; b < kSpecBuckets; ++b) {
     std::printf("%%s[", b ? "," : "");
@@ -168,3 +176,38 @@ def test_walk_replays_the_sequential_chain(tables):
             n = c
         assert all(v < S for v in visited)
         assert used == left or len(visited) == used
+
+
+def test_parallel_path_equals_the_walk(tables):
+    """The in-wave resolution (spec_on_path / spec_path_round): node n is on the
+    realized path iff every ancestor decided the way n's path goes; the path's
+    nodes, in index order, are exactly the walk's visited nodes, and the last
+    accepted one is the walk's new state."""
+    rng = np.random.default_rng(7)
+    for _ in range(600):
+        b = int(rng.integers(0, len(tables["p"])))
+        S = int(rng.choice([1, 2, 4, 8, 16, 32, 64]))
+        left = int(rng.integers(1, 80))
+        tree = tables["trees"][b]
+        anc = [(int(a), int(e)) for a, e in tables["anc"][b]]
+        acc = 0
+        for n in range(S):
+            if tree[n][3] < left and rng.random() < rng.random():
+                acc |= 1 << n
+        # the walk
+        n, used, visited, win = 0, 0, [], -1
+        while True:
+            a = (acc >> n) & 1
+            visited.append(n)
+            if a:
+                win = n
+            used += 1
+            c = tree[n][2] if a else tree[n][1]
+            if used >= left or c < 0 or c >= S:
+                break
+            n = c
+        # the parallel form
+        path = [m for m in range(S) if tree[m][3] < left and ((acc ^ anc[m][1]) & anc[m][0]) == 0]
+        assert path == visited, (b, S, left)
+        pa = [m for m in path if (acc >> m) & 1]
+        assert (pa[-1] if pa else -1) == win

@@ -295,6 +295,41 @@ case "$1" in
       done
     done
     ;;
+  final2)
+    # the exact tree the round ends on: the suite, smoke(), the default bench line
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_final2.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } &&
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_final2.log 2>&1 &&
+    timeout -k 10 600 python bench.py > $O/bench_default_final2.json 2> $O/bench_default_final2.err
+    ;;
+  s17)
+    # config 1 on the device path (one chain, linear G) with speculation trees;
+    # the Lorenz-63 loop unrolled by 8: its parity tests on the variant, then
+    # config 2 against the product (4), interleaved
+    V=ip_mcmc_amd/lib/variants/l63u8/libipmc.so
+    timeout -k 10 300 python tools/probes/cfg1_e2e.py > $O/cfg1_e2e_final.jsonl &&
+    IPMC_LIB_PATH=$V timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests \
+        -m gpu -k "small or cfg2 or l63 or L63 or dense_prior or speculative" > $O/pytest_l63u8.log 2>&1 &&
+    for i in 1 2; do
+      for lib in "" "$V"; do
+        IPMC_LIB_PATH=$lib timeout -k 10 200 python tools/config_bench.py cfg2@16384 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product_u4}'))) for l in sys.stdin]" >> $O/l63_unroll_ab3.jsonl || exit 1
+      done
+    done
+    ;;
+  s18)
+    # in-wave trees resolved in parallel (small_spec_kernel) and the Lorenz-63
+    # loop unrolled by 8: the speculative parity tests, config 1 on the device
+    # path, config 2, then the whole suite
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests \
+        -m gpu -k "small or cfg2 or l63 or L63 or dense_prior or speculative or linear or sampler" > $O/pytest_s18_spec.log 2>&1 &&
+    timeout -k 10 300 python tools/probes/cfg1_e2e.py > $O/cfg1_e2e_s18.jsonl &&
+    timeout -k 10 200 python tools/config_bench.py cfg2@16384 > $O/cfg2_s18.jsonl &&
+    timeout -k 10 200 python examples/lorenz63_config2.py > $O/example_l63_cfg2_s18.jsonl &&
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_s18.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } &&
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s18.log 2>&1
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
