@@ -439,11 +439,21 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
   // (~7 steps per round at S = 16); a chain accepting nothing gets the reject
   // chain (S steps per round).
   SpecGuess guess(spec_accept_prior(s, chain));
+  // this lane's node of the current tree, reloaded only when the tree changes
+  // (a table load per round is most of a linear round's latency)
+  int ctb = -1, maxlvl = 0;
+  SpecNode nd{};
+  unsigned long long nanc = 0, nedge = 0;
   while (st < s.n_steps) {
     const int64_t left = s.n_steps - st;
     const int tb = guess.bucket();
-    const SpecNode nd = kSpecTrees.nd[tb][sub];
-    const int maxlvl = kSpecTrees.maxlvl[tb][S];
+    if (tb != ctb) {  // uniform per group
+      nd = kSpecTrees.nd[tb][sub];
+      maxlvl = kSpecTrees.maxlvl[tb][S];
+      nanc = kSpecTrees.anc[tb][sub];
+      nedge = kSpecTrees.edge[tb][sub];
+      ctb = tb;
+    }
     const bool act = nd.depth < left;  // this node's step is in the launch
     const int64_t tt = st + nd.depth;
     if constexpr (PRE) {
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(kSpecBlock) void small_spec_kernel(const ipmc_model
     const unsigned long long accm = (__ballot(acc) >> gbase) & gmask;
     const unsigned long long okm = (__ballot(ok) >> gbase) & gmask;
     // the walk resolved in parallel: each lane tests whether its node is on the path
-    const unsigned long long path = (__ballot(spec_on_path(tb, sub, accm, act)) >> gbase) & gmask;
+    const unsigned long long path = (__ballot(act && ((accm ^ nedge) & nanc) == 0) >> gbase) & gmask;
     const SpecRound rd = spec_path_round(path, accm, okm);
     const T phf = __shfl(phv, gbase + (rd.win >= 0 ? rd.win : 0), 64);
     if (sub == 0 && (s.sum_u || (s.sample_every > 0 && clk.next < st + rd.used))) {

@@ -330,6 +330,16 @@ case "$1" in
         > $O/pytest_gpu_s18.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } &&
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s18.log 2>&1
     ;;
+  s19)
+    # the small speculative kernel keeping its tree node across rounds
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests \
+        -m gpu -k "small or cfg2 or l63 or L63 or dense_prior or speculative or linear or sampler" > $O/pytest_s19_spec.log 2>&1 &&
+    timeout -k 10 300 python tools/probes/cfg1_e2e.py > $O/cfg1_e2e_s19.jsonl &&
+    timeout -k 10 200 python tools/config_bench.py cfg2@16384 > $O/cfg2_s19.jsonl &&
+    { timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
+        > $O/pytest_gpu_s19.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } &&
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s19.log 2>&1
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
