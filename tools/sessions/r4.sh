@@ -340,6 +340,16 @@ case "$1" in
         > $O/pytest_gpu_s19.log 2>&1; rc=$?; echo "pytest rc=$rc"; [ $rc -eq 0 ]; } &&
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s19.log 2>&1
     ;;
+  s20)
+    # config 2's SQ pass on the final kernel (unroll 8, parallel walk)
+    SQS="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+    timeout -s KILL 90 rocprofv3 --pmc $SQS --kernel-trace --output-format csv -d $O/sq_cfg2_final/f64 -o run -- \
+        python tools/config_bench.py cfg2@16384!f64 > /dev/null &&
+    timeout -s KILL 90 rocprofv3 --pmc $SQS --kernel-trace --output-format csv -d $O/sq_cfg2_final/f32 -o run -- \
+        python tools/config_bench.py cfg2@16384!f32 > /dev/null &&
+    python tools/sq_summarize.py $O/sq_cfg2_final/f64 small_spec_kernel > $O/sq_cfg2_final_f64.json &&
+    python tools/sq_summarize.py $O/sq_cfg2_final/f32 small_spec_kernel > $O/sq_cfg2_final_f32.json
+    ;;
   dbg)
     timeout -k 10 300 python tools/probes/spec_tree_debug.py > $O/spec_tree_debug.txt 2>&1 &&
     IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/burshfl/libipmc.so timeout -k 10 300 python tools/probes/spec_tree_debug.py \
