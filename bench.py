@@ -74,12 +74,12 @@ class Problem:
 
     def reference_arith(self):
         """The same problem with the forward map in REFERENCE arith (no FMA, the
-        reference's operation order; Lorenz-96 only)."""
+        reference's operation order: lorenz.py:77-81, rusanov.py:62-96)."""
         import copy
 
         p = copy.copy(self)
-        o = self.op
-        p.op = Lorenz96Operator(o.K, forcing_mean=o.theta0, x0=o.x0, dt=o.dt, n_steps=o.n_steps, arith="reference")
+        p.op = copy.copy(self.op)
+        p.op.arith, p.op._cache = "reference", {}
         return p
 
 
@@ -110,7 +110,72 @@ def make_problem(key):
         return Problem(key, "lorenz96_d256_rk4_10000_pcn", op, y, 0.1, np.ones(d), 0.2, 1 << 20, 30 * d * n, 30 / 40,
                        4, 1, "synthetic (forcing-field inverse problem, d=256, y = G(0.5 sin(2 pi k/256)) + "
                        "N(0, 0.1^2), seed 3; prior N(0, I); u_0 = 0)")
+    if key == "cfg3_mixing":
+        # the headline's shape and kernel on a posterior the chains sample: the
+        # reference's noise recipe (lorenz_mcmc.py:100-112, gamma = r sd(X_k))
+        # at r = 2, tools/posterior_agreement.py:91-100
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import posterior_agreement as PA
+
+        d, n = 40, 2000
+        y, gamma, _, x0 = PA.problem(d, n, 2.0)
+        op = Lorenz96Operator(d, forcing_mean=8.0, x0=x0, dt=0.005, n_steps=n)
+        return Problem(key, "lorenz96_d40_rk4_2000_pcn_mixing", op, y, gamma, np.ones(d), 0.2, 65536, 30 * d * n,
+                       30 / 40, 200, 10, f"synthetic (forcing-field problem, gamma = 2 sd(X_k) = {gamma:.3f}; "
+                                         "prior N(0, I); u_0 = 0)")
     raise SystemExit(f"unknown workload {key}")
+
+
+CFG5_PARITY_NOTE = ("no floor: 10 000 RK4 steps = 50 time units run far past Lorenz-96's predictability horizon "
+                    "(rounding differences grow ~e^(1.7 t)), so G in any two arithmetics are unrelated and paired "
+                    "streams part at the first steps; bit-exact streams at config 5 are REFERENCE arith's (GPU == "
+                    "oracle, tests/test_gpu_paired_streams.py; its rate: extra.configs.cfg5.reference_f64), the "
+                    "precision claim the stationary fp32/fp64 tolerance (tests/test_gpu_tolerance.py)")
+
+
+def _hist(x, edges):
+    c, _ = np.histogram(x, bins=edges)
+    return {"edges": [int(e) for e in edges], "counts": [int(v) for v in c]}
+
+
+def paired_streams(prob, chains, steps, dtype, dev):
+    """The accept/reject index streams of the benched FMA forward map against
+    REFERENCE arith (the reference's operation order, pinned bit for bit to the
+    reference fixtures: lorenz.py:77-81, rusanov.py:62-96), on `prob` itself:
+    the same seed, u_0 = 0 and global chain ids, so both arms draw the same
+    proposals and uniforms (accepter.py:59-62,121-122's rule on the same
+    numbers); only G's rounding differs.  One pCN step per launch; after each
+    the accept counters give every chain's decision.  A chain whose decisions
+    agree at every step has the same states bit for bit in both arms (the
+    proposal never reads G), which is checked.  Returns the record."""
+    arms = [Workload(p, chains, 0, dtype, dev) for p in (prob, prob.reference_arith())]
+    dec = []
+    for w in arms:
+        D = torch.empty((steps, chains), dtype=torch.int8, device=dev)
+        prev = w.acc.clone()
+        for t in range(steps):
+            w.step(1)
+            D[t] = (w.acc - prev).to(torch.int8)
+            prev.copy_(w.acc)
+        dec.append(D)
+    torch.cuda.synchronize(dev)
+    diff = dec[0] != dec[1]
+    div = diff.any(dim=0)
+    first = torch.argmax(diff.to(torch.int8), dim=0)[div].cpu().numpy()
+    same = ~div
+    ident = float(same.float().mean().item())
+    state_eq = bool(torch.equal(arms[0].u[same], arms[1].u[same]))
+    phf, phr = arms[0].phi[same].double(), arms[1].phi[same].double()
+    rel = float(((phf - phr).abs() / phr.abs().clamp_min(1e-300)).max().item()) if phf.numel() else None
+    edges = [e for e in sorted({0, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, steps}) if e <= steps]
+    return {"workload": prob.name, "chains": chains, "steps": steps, "dtype": "f64" if dtype == torch.float64 else
+            "f32", "identical_accept_stream_frac": ident, "diverged_chains": int(div.sum().item()),
+            "first_divergence_step_hist": _hist(first, edges),
+            "accept_rate_fma": float(dec[0].float().mean().item()),
+            "accept_rate_reference": float(dec[1].float().mean().item()),
+            "identical_chains_states_bit_equal": state_eq, "identical_chains_phi_max_rel_diff": rel,
+            "how": "same seed, u_0 = 0 and chain ids in both arms; one pCN step per launch; decisions from the accept "
+                   "counters; FMA arith (benched) vs REFERENCE arith (the reference's operation order)"}
 
 
 # ------------------------------------------------------------ kernel leg
@@ -336,6 +401,10 @@ def config_line(key, dev, world, steps=None, warmup=None, chains=None):
     out = {"workload": prob.name, "f64": rec64, "flop_per_chain_step": prob.flop,
            "tflops_f64": total * prob.flop * st / rec64["wall_s"] / 1e12}
     if key == "cfg5":
+        # REFERENCE arith: the arithmetic whose accept streams are the reference's at this length
+        recr = timed_run(prob.reference_arith(), np.float64, dev, total, st, wu, world, gather=gather)[0]
+        out["reference_f64"] = recr
+        out["tflops_reference_f64"] = total * prob.flop * st / recr["wall_s"] / 1e12
         rec32, r32 = timed_run(prob, np.float32, dev, total, st, wu, world, gather=gather, seed=3)
         out["f32"] = rec32
         out["tflops_f32"] = total * prob.flop * st / rec32["wall_s"] / 1e12
@@ -428,6 +497,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the short cfg4 / cfg5 runs in extra.configs")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the paired FMA / REFERENCE accept-stream runs (parity.*; N = 1 only)")
     ap.add_argument("--pmc-file", default=None,
                     help="a tools/pmc_summarize.py record of this box's PMC passes for roofline.traffic (default: the "
                          "newest committed profiles/r*/pmc_l96_<dtype>.json of the same kernel and layout)")
@@ -518,6 +589,23 @@ def main():
              "kernel_note": "device-resident state, raw ipmc_pcn_sweep launches of steps_per_launch steps, HIP "
                             "events on the launch stream (the roofline's kernel time); no H2D / D2H / gather",
              "run_e2e_moments": e2e}
+    parity = {}
+    if not args.no_parity and world == 1 and not args.kernel_only:
+        # north_star's bit-exact accept streams, for the arithmetic value is
+        # timed in: paired FMA / REFERENCE runs of the benched problems
+        # (DESIGN.md §6 states and tests/test_gpu_paired_streams.py asserts the floors)
+        pp = paired_streams(prob, per_rank, max(steps, 200), tdt, dev)
+        log(f"paired FMA/REFERENCE accept streams ({args.workload}): {pp['identical_accept_stream_frac']:.5f} "
+            f"identical over {pp['steps']} steps")
+        parity["paired_identical_accept_frac"] = pp["identical_accept_stream_frac"]
+        parity[args.workload] = pp
+        if args.workload == "cfg3" and not args.no_configs:
+            for key, ch, st in (("cfg4", 16384, 200), ("cfg5", 16384, 100)):
+                pp = paired_streams(make_problem(key), ch, st, tdt, dev)
+                log(f"paired FMA/REFERENCE accept streams ({key}): {pp['identical_accept_stream_frac']:.5f}")
+                parity[key] = pp
+        if "cfg5" in parity:
+            parity["cfg5"]["note"] = CFG5_PARITY_NOTE
     if not args.no_extra and args.workload == "cfg3":
         # one-step launches: 40 steps are plenty; speculative launches (small
         # shards) are timed over the headline's steps, as short ones are slow
@@ -545,6 +633,19 @@ def main():
         extra["reference_arith_kernel_ms"] = k3
         extra["reference_arith_kernel_tflops"] = per_rank * per_launch * prob.flop / (k3 * 1e-3) / 1e12
         del w3
+        # REFERENCE arith end to end: the same timed region as value
+        er = timed_run(pref, ndt, dev, total_chains, steps, 2, world, gather=gather_mode)[0]
+        log(f"reference arith end to end: {er['pcn_steps_per_s'] / 1e6:.2f} M steps/s")
+        parity["reference_arith_value"] = er["pcn_steps_per_s"]
+        parity["reference_arith_run_e2e_moments"] = er
+        # the headline's shape and kernel on a posterior the chains sample
+        # (the rate should not depend on acceptance)
+        pmix = make_problem("cfg3_mixing")
+        em = timed_run(pmix, ndt, dev, total_chains, steps, 2, world, gather=gather_mode)[0]
+        log(f"mixing posterior end to end: {em['pcn_steps_per_s'] / 1e6:.2f} M steps/s, "
+            f"{em['accept_rate']:.3f} accepted")
+        extra["mixing_posterior"] = dict(em, workload=pmix.name, data=pmix.data, over_value=em["pcn_steps_per_s"] / value,
+                                         accept_rate_value=accept_rate)
         if world > 1:  # weak scaling beside the strong line: 65 536 chains per GPU
             wk, _ = timed_run(prob, ndt, dev, world * CHAINS_PER_GPU, min(steps, 40), 2, world, gather=gather_mode)
             extra["weak_scaling"] = {"pcn_steps_per_s": wk["pcn_steps_per_s"], "total_chains": world * CHAINS_PER_GPU,
@@ -636,6 +737,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "accept_rate": accept_rate,
+            "parity": parity or None,
             "final_gather": gather,
             "extra": extra,
         }

@@ -36,8 +36,8 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"libipmc_host.so not found at {LIB_PATH}; build it first "
-                               "(python -c 'import __graft_entry__ as g; g.build()')")
+            raise RuntimeError(f"libipmc_host.so not found at {LIB_PATH}; build it first: "
+                               "make -C ip_mcmc_amd/csrc host (g++ only, no ROCm needed)")
         h = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(h, name)

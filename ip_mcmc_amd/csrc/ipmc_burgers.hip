@@ -20,6 +20,8 @@
 namespace ipmc {
 
 constexpr int kBurBlock = 256;
+// block-wide rounds index kSpecTrees.nd[tb][slot] with slot < kBurBlock / GS
+static_assert(kBurBlock <= kSpecNodes, "block-wide speculation slots index the spec-tree tables");
 
 // Rusanov flux F = ½(f(a)+f(b)) − ½·max(|a|,|b|)·(b−a), f(w) = w²/2
 // (rusanov.py:92-96), REFERENCE arith: the reference's operation order.
@@ -550,9 +552,40 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
     };
     SpecRound rd;
     T phf;
+    bool walked_sums = false;
     if (G <= 64) {
       accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
       okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
+#ifdef IPMC_PROBE_WALK_SHFL
+      // round 4's first form, kept as a build variant for the root-cause probe
+      // (tools/probes/walk_shfl_probe.py): the running sums taken inside the
+      // walk, each settled step's state read from its slot by __shfl
+      if (s.sum_u && s.sample_every == 0) {
+        walked_sums = true;
+        const bool sums = r == 0;
+        RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
+                          sums ? 3 : 0);
+        rd = spec_walk(S, left, node, [&](int, int la) {
+          T vq[3];
+#if IPMC_PROBE_WALK_SHFL == 2  // the read under the first lane's branch: its source lanes are inactive
+          if (sums) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * GS, 64);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
+          }
+#else  // every lane of the chain reads
+#pragma unroll
+          for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * GS, 64);
+          if (sums) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
+          }
+#endif
+        });
+        if (sums) rsum.store();
+      } else
+#endif
       rd = spec_walk(S, left, node, [](int, int) {});
       phf = __shfl(phv, cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
     } else {
@@ -582,7 +615,7 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
     if (G > 64) slot_v(rd.win >= 0 ? rd.win : 0, vf);
-    if (s.sum_u || s.sample_every > 0) {  // uniform per chain (only lane r == 0 keeps the clock)
+    if ((s.sum_u || s.sample_every > 0) && !walked_sums) {  // uniform per chain (only lane r == 0 keeps the clock)
       // the states after each settled step, in step order: the same walk again
       const bool sums = s.sum_u && r == 0;
       RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,

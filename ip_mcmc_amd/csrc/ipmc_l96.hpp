@@ -54,7 +54,9 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
       x[j] = madd<FM>(c, acc[j], x[j]);
       ob[j] = ob[j] + x[j];
     } else {
-      acc[j] = madd<FM>(two, k, acc[j]);
+      // 2k is exact, so fma(2, k, acc) rounds once exactly as the reference
+      // order's acc + 2k does: fused in both arithmetic modes (one op, not two)
+      acc[j] = madd<true>(two, k, acc[j]);
       xs[j] = madd<FM>(c, k, x[j]);
     }
   }
@@ -101,6 +103,8 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
 
 constexpr int kL96Block = 256;
 static_assert(kL96Block == kL96SpecBlockLanes, "block-wide speculation spans one block");
+// block-wide rounds index kSpecTrees.nd[tb][slot] with slot < kL96Block / LPC
+static_assert(kL96Block <= kSpecNodes, "block-wide speculation slots index the spec-tree tables");
 
 // LDS staging for the in-order misfit / regularizer sums of wide groups
 // (LPC >= 8, group_sumsq); one element otherwise.
@@ -128,17 +132,26 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
 // RK loop keeps 5 arrays of M values live (x, F, time-average, k-sum, stage;
 // l96_stage consumes each rate as it is computed), the proposal / accept stage
 // ~40 registers of addressing / RNG / loop state around it.  The target is
-// sized for 6 arrays (fp64 M = 20 then takes all 256 VGPRs FP64 operands can
-// address, i.e. two waves, without scratch).
+// sized for 6 arrays (fp64 M = 20: one wave, where the FMA kernel takes 271
+// registers -- 256 VGPRs and 15 AGPRs -- without scratch; it issues in every
+// VALU slot at one wave per SIMD).
 // (fp32 one chain per lane group: the compiler's SLP packing needs ~96; every
 // variant gets at least 104 registers, i.e. at most 4 waves, since the
 // proposal / accept stage spills below that: 20-56 B per lane at 5 waves for
 // M <= 5, e.g. d=40 at 8 lanes per chain.)
-template <typename T, int M>
+// REFERENCE arith in fp64 at 17-20 components per lane (the headline's d=40 on
+// 2 lanes): held to two waves.  Left free (one wave), the compiler took 258
+// registers, one wave per SIMD; at two it spills 12 B per lane outside the RK
+// loop and the headline kernel runs 5.24 -> 4.89 ms (12.5 -> 13.4 M pCN
+// steps/s; profiles/r5/arith_waves_ab.jsonl).  The FMA kernel gains 2 % the
+// same way but spills 80 B per lane, as much HBM traffic as the compulsory
+// bytes: it stays at one wave.
+template <typename T, int M, bool FM = true>
 constexpr int l96_waves_per_simd() {
 #ifdef IPMC_L96_WAVES  // occupancy experiments (tools/)
   return IPMC_L96_WAVES;
 #endif
+  if constexpr (!FM && sizeof(T) == 8 && M >= 17 && M <= 20) return 2;
   constexpr int want = 6 * M * (int)(sizeof(T) / 4) + (sizeof(T) == 8 ? 40 : 96);
   constexpr int regs = want < 104 ? 104 : want;
   constexpr int w = 512 / regs;
@@ -163,7 +176,7 @@ constexpr int l96_pk_waves_per_simd() {
 
 // n_steps pCN steps per launch; u / Φ(u) / accept counts updated in place.
 template <typename T, int D, int LPC, bool FM>
-__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void l96_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
+__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) void l96_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
   constexpr int M = D / LPC;
   constexpr bool IL = (LPC == 8);  // interleaved groups of 8 (group_vlane)
   __shared__ T vpark[M][kL96Block];  // proposal parked in LDS while G runs
@@ -563,7 +576,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
 
 // G(u) or Φ(u) for n parameter vectors (no proposal): out = g [n, D] or phi [n].
 template <typename T, int D, int LPC, bool FM, bool PHI>
-__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC>())) void l96_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
+__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) void l96_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
                                                               const T* __restrict__ yin,
                                                               const T* __restrict__ ginvin, T* __restrict__ out) {
   constexpr int M = D / LPC;

@@ -24,12 +24,13 @@ __device__ __forceinline__ void l63_rhs(T sg, T rh, T bb, const T (&s)[3], T (&o
   }
 }
 
-// RK4 steps per loop iteration.  Config 2 runs one wave per SIMD, where a
-// round is one forward map at a single wave's issue rate: four steps per
-// iteration let the scheduler overlap one step's moment updates and k-sum
-// with the next step's right-hand side (same operations, same bits): config 2
-// 455 -> 501 M steps/s in f64, 549 -> 604 M in fp32 against the compiler's
-// own choice (profiles/r4/l63_unroll_ab.jsonl).  0: the compiler's choice.
+// RK4 steps per loop iteration (default 8).  Config 2 runs one wave per SIMD,
+// where a round is one forward map at a single wave's issue rate: unrolled
+// steps let the scheduler overlap one step's moment updates and k-sum with the
+// next step's right-hand side (same operations, same bits): config 2 453 ->
+// 498 M steps/s in f64, 549 -> 615 M in fp32 by 8 against the compiler's own
+// choice (by 4: 497 / 604 M; profiles/r4/l63_unroll_ab2.jsonl,
+// l63_unroll_ab3.jsonl).  0: the compiler's choice.
 #ifndef IPMC_L63_UNROLL
 #define IPMC_L63_UNROLL 8
 #endif

@@ -36,6 +36,9 @@ namespace ipmc {
 
 constexpr int kSpecBuckets = 23;
 constexpr int kSpecNodes = 256;
+// SpecNode.depth / .lvl and maxlvl are uint8_t: a node index, depth or level
+// must fit in 8 bits
+static_assert(kSpecNodes <= 256, "spec-tree node fields are uint8_t");
 constexpr double kSpecGridP[kSpecBuckets] = {
     0.0,         1.0 / 128,   1.0 / 64,    1.0 / 32,    1.0 / 16,     2.0 / 16,   3.0 / 16,   4.0 / 16,
     5.0 / 16,    6.0 / 16,    7.0 / 16,    8.0 / 16,    9.0 / 16,     10.0 / 16,  11.0 / 16,  12.0 / 16,

@@ -1,4 +1,4 @@
-"""Multi-process chain sharding on CPU (gloo, world_size 2 and 3).
+"""Multi-process chain sharding on CPU (gloo, world_size 2, 3 and 8).
 
 Each rank owns a contiguous block of global chain ids (shard.chain_range),
 advances it with the CPU oracle (the per-rank compute stand-in: on the GPU box
@@ -141,7 +141,7 @@ def _lin_sampler_factory():
     return make
 
 
-def _sharded_worker(rank, world, port, out_path, keep, gather="all"):
+def _sharded_worker(rank, world, port, out_path, keep, gather="all", n_total=C_TOTAL):
     import sys
 
     sys.path.insert(0, REPO)
@@ -150,7 +150,7 @@ def _sharded_worker(rank, world, port, out_path, keep, gather="all"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    u0 = 0.1 * np.random.default_rng(1).normal(size=(C_TOTAL, 4))
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(n_total, 4))
     res = run_sharded(_lin_sampler_factory(), u0, n_samples=6, burn_in=9, sample_interval=4, keep=keep,
                       gather=gather)
     assert res["world"] == world and res["sampler"].last_path == "host"
@@ -197,6 +197,30 @@ def test_run_sharded_mean_by_rank_sequential_sum(tmp_path):
     for key in ("mean", "phi", "accepts"):
         assert np.array_equal(got[key], one[key]), key
     assert got["sum_u"].shape[0] == 12  # rank 1's own block of chain_range(37, 1, 3)
+
+
+@pytest.mark.parametrize("n_total", [1003, 5])
+@pytest.mark.parametrize("gather", ["all", "mean"])
+def test_run_sharded_world_8_uneven(tmp_path, gather, n_total):
+    """An 8-rank rehearsal of the node (gloo): 1 003 chains (ranks of 126 and
+    125) and 5 chains (three ranks with none).  The gathered Φ and accept
+    counts and the posterior mean equal one process's bit for bit in both
+    gather modes; gather='all' also the states and sums."""
+    from ip_mcmc_amd.shard import chain_range, run_sharded
+
+    out = str(tmp_path / "w8.npz")
+    mp.start_processes(_sharded_worker, args=(8, _free_port(), out, "moments", gather, n_total), nprocs=8,
+                       start_method="spawn")
+    got = np.load(out)
+    u0 = 0.1 * np.random.default_rng(1).normal(size=(n_total, 4))
+    one = run_sharded(_lin_sampler_factory(), u0, n_samples=6, burn_in=9, sample_interval=4, keep="moments")
+    keys = ("mean", "phi", "accepts") + (("u", "sum_u", "sum_u2") if gather == "all" else ())
+    for key in keys:
+        assert np.array_equal(got[key], one[key]), key
+    if gather == "mean":  # rank 1's own rows only
+        a, b = chain_range(n_total, 1, 8)
+        assert np.array_equal(got["sum_u"], one["sum_u"][a:b])
+    assert one["accepts"].sum() > 0
 
 
 def _sharded_file_worker(rank, world, port, prefix):

@@ -1,4 +1,8 @@
-"""Debug: which speculative ts / Burgers sweep sums differ from the oracle."""
+"""Debug: which speculative ts / Burgers sweep sums differ from the oracle.
+
+  [IPMC_LIB_PATH=variant] python tools/probes/spec_tree_debug.py [case-prefix ...]
+  (e.g. `bur128` with the IPMC_PROBE_WALK_SHFL variant: round 4's failing form)
+"""
 import os
 import sys
 
@@ -22,7 +26,10 @@ for K, J, arith in ((6, 4, "fma"), (3, 1, "reference"), (11, 2, "fma")):
 for N, arith in ((128, "reference"), (256, "fma")):
     op = BurgersOperator(N=N, dt_mode="cfl", T=0.2, arith=arith)
     cases.append((f"bur{N}", op, (1, 0, 2, 4, 16) if N == 128 else (1, 0, 2, 8)))
+only = sys.argv[1:]
 for name, op, widths in cases:
+    if only and not any(name.startswith(o) for o in only):
+        continue
     for scale in (0.2, 3.0):
         U0, phi0, y, ginv, sq = T._problem(op, 19, dtype, orc, seed=3)
         ginv = ginv * scale
