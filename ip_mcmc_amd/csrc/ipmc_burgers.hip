@@ -542,51 +542,21 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
     const bool acc = ok && (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
     // one bit per slot (its first lane, bit slot*GS of the chain's lanes)
     const SpecNode* tree = kSpecTrees.nd[tb];
-    unsigned long long accm = 0, okm = 0;  // G <= 64: the chain's bits
-    const int kids = spec_pack_children(nd);
-    // G <= 64: node n's children from its slot's lanes; a block-wide chain: from the table
+    unsigned long long accm = 0, path = 0;  // G <= 64: the chain's bits, one per slot
+    // a block-wide chain's node n from the table and the waves' ballots in LDS
     auto node = [&](int n) {
-      if (G <= 64) return spec_step_packed(__shfl(kids, cbase + n * GS, 64), n, GS, accm, okm);
       const int bit = n * GS;
       return spec_step_bits(tree, n, 0, bmask[0][bit >> 6] >> (bit & 63), bmask[1][bit >> 6] >> (bit & 63));
     };
     SpecRound rd;
     T phf;
-    bool walked_sums = false;
     if (G <= 64) {
-      accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
-      okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-#ifdef IPMC_PROBE_WALK_SHFL
-      // round 4's first form, kept as a build variant for the root-cause probe
-      // (tools/probes/walk_shfl_probe.py): the running sums taken inside the
-      // walk, each settled step's state read from its slot by __shfl
-      if (s.sum_u && s.sample_every == 0) {
-        walked_sums = true;
-        const bool sums = r == 0;
-        RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
-                          sums ? 3 : 0);
-        rd = spec_walk(S, left, node, [&](int, int la) {
-          T vq[3];
-#if IPMC_PROBE_WALK_SHFL == 2  // the read under the first lane's branch: its source lanes are inactive
-          if (sums) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * GS, 64);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
-          }
-#else  // every lane of the chain reads
-#pragma unroll
-          for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * GS, 64);
-          if (sums) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) rsum.add(j, la >= 0 ? (double)vq[j] : (double)ur[j]);
-          }
-#endif
-        });
-        if (sums) rsum.store();
-      } else
-#endif
-      rd = spec_walk(S, left, node, [](int, int) {});
+      // the walk resolved in parallel (spec_on_path, as ipmc_l96.hpp): no
+      // cross-lane read inside a data-dependent loop
+      accm = spec_slot_bits((__ballot(acc && c.sub == 0) >> cbase) & gmask, S, GS);
+      const unsigned long long okm = spec_slot_bits((__ballot(ok && c.sub == 0) >> cbase) & gmask, S, GS);
+      path = spec_slot_bits((__ballot(spec_on_path(tb, slot, accm, act) && c.sub == 0) >> cbase) & gmask, S, GS);
+      rd = spec_path_round(path, accm, okm);
       phf = __shfl(phv, cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
     } else {
       const int t = threadIdx.x;
@@ -615,12 +585,12 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], cbase + (rd.win >= 0 ? rd.win : 0) * GS, 64);
     if (G > 64) slot_v(rd.win >= 0 ? rd.win : 0, vf);
-    if ((s.sum_u || s.sample_every > 0) && !walked_sums) {  // uniform per chain (only lane r == 0 keeps the clock)
+    if (s.sum_u || s.sample_every > 0) {  // uniform per chain (only lane r == 0 keeps the clock)
       // the states after each settled step, in step order: the same walk again
       const bool sums = s.sum_u && r == 0;
       RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
                         sums ? 3 : 0);
-      spec_replay(rd.used, node, [&](int q, int la) {
+      auto visit = [&](int q, int la) {
         T vq[3];
         slot_v(la >= 0 ? la : 0, vq);
         if (r == 0) {
@@ -636,7 +606,9 @@ __global__ __launch_bounds__(kBurBlock) void burgers_sweep_kernel(const ipmc_mod
             for (int j = 0; j < 3; ++j) so[j] = la >= 0 ? vq[j] : ur[j];
           }
         }
-      });
+      };
+      if (G <= 64) spec_path_replay(path, accm, visit);
+      else spec_replay(rd.used, node, visit);
       if (sums) rsum.store();
     }
     if (G > 64) __syncthreads();  // bmask / vpk are rewritten next round

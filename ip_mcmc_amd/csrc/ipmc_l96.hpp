@@ -146,12 +146,15 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
 // steps/s; profiles/r5/arith_waves_ab.jsonl).  The FMA kernel gains 2 % the
 // same way but spills 80 B per lane, as much HBM traffic as the compulsory
 // bytes: it stays at one wave.
+#ifndef IPMC_L96_PARK  // A/B: the sequential sweep's lane state parked in LDS across G, fp64 M 17-20 at two waves
+#define IPMC_L96_PARK 0
+#endif
 template <typename T, int M, bool FM = true>
 constexpr int l96_waves_per_simd() {
 #ifdef IPMC_L96_WAVES  // occupancy experiments (tools/)
   return IPMC_L96_WAVES;
 #endif
-  if constexpr (!FM && sizeof(T) == 8 && M >= 17 && M <= 20) return 2;
+  if constexpr ((!FM || IPMC_L96_PARK) && sizeof(T) == 8 && M >= 17 && M <= 20) return 2;
   constexpr int want = 6 * M * (int)(sizeof(T) / 4) + (sizeof(T) == 8 ? 40 : 96);
   constexpr int regs = want < 104 ? 104 : want;
   constexpr int w = 512 / regs;
@@ -181,21 +184,49 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) 
   constexpr bool IL = (LPC == 8);  // interleaved groups of 8 (group_vlane)
   __shared__ T vpark[M][kL96Block];  // proposal parked in LDS while G runs
   __shared__ T stage[l96_stage_len<M, LPC>()];
+#if IPMC_L96_PARK
+  __shared__ T phpark[kL96Block];  // Φ(u) parked in LDS while G runs
+#endif
   const int lane = threadIdx.x & 63;
-  const int64_t tid = (int64_t)blockIdx.x * kL96Block + group_vlane<LPC, IL>(threadIdx.x);
-  const int64_t chain = tid / LPC;
-  const int sub = (int)(tid % LPC);
-  if (chain >= s.n_chains) return;  // whole lane groups leave together
-  const uint64_t gid = (uint64_t)(s.chain_offset + chain);
-  const int c0 = sub * M;
-  T* __restrict__ u = (T*)s.u + chain * D + c0;
+  // the lane's chain, component block and addresses, from the thread index;
+  // with IPMC_L96_PARK recomputed every pCN step behind an opaque copy of the
+  // index, so none of it stays live across G
+  struct Lane {
+    int64_t chain;
+    int sub, c0;
+    uint64_t gid;
+    T* u;
+  };
+  auto lane_state = [&](int tx) {
+    Lane l;
+    const int64_t tid = (int64_t)blockIdx.x * kL96Block + group_vlane<LPC, IL>(tx);
+    l.chain = tid / LPC;
+    l.sub = (int)(tid % LPC);
+    l.c0 = l.sub * M;
+    l.gid = (uint64_t)(s.chain_offset + l.chain);
+    l.u = (T*)s.u + l.chain * D + l.c0;
+    return l;
+  };
+  Lane L0 = lane_state(threadIdx.x);
+  if (L0.chain >= s.n_chains) return;  // whole lane groups leave together
   const T beta = (T)s.beta, contr = (T)s.contraction, h = (T)m.dt;
   T* phi = (T*)s.phi;
-  T phu = phi[chain];
+  T phu = phi[L0.chain];
   const bool rw = (s.proposal == IPMC_PROPOSAL_RW);
   int nacc = 0, ncalls = 0;  // per launch (n_steps <= INT32_MAX, checked by the API)
   for (int64_t st = 0; st < s.n_steps; ++st) {
     const uint64_t step = s.step0 + (uint64_t)st;
+#if IPMC_L96_PARK
+    int tx = threadIdx.x;
+    asm volatile("" : "+v"(tx));
+    const Lane L = lane_state(tx);
+#else
+    const Lane& L = L0;
+#endif
+    const int64_t chain = L.chain;
+    const int c0 = L.c0;
+    const uint64_t gid = L.gid;
+    T* __restrict__ u = L.u;
     // Opaque per-step offset: keeps the loop-invariant per-component constants
     // (theta0, x0, y, 1/gamma, sqrt C) from being hoisted into 5*M VGPRs for
     // the whole launch; they are re-read from L1/L2 once per pCN step instead.
@@ -217,14 +248,28 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) 
                         : (T)0;
 #pragma unroll
       for (int j = 0; j < M; ++j) vpark[j][threadIdx.x] = v[j];
+#if IPMC_L96_PARK
+      phpark[threadIdx.x] = phu;
+#endif
       T phv = l96_potential<T, M, LPC, FM, IL>(v, (const T*)m.theta0 + cl, (const T*)m.x0 + cl, (const T*)s.y + cl,
                                            (const T*)s.gamma_inv + cl, h, m.n_steps, lane, stage);
       if (s.reg_scale) phv = phv + reg;  // I(v) = Φ(v) + regularizer (accepter.py:106)
       // memory clobber: re-read v from LDS instead of keeping it live in VGPRs across G
       asm volatile("" ::: "memory");
-      if (pcn_accept<T>(phu, phv, s.seed, gid, step)) {
+#if IPMC_L96_PARK
+      phu = phpark[threadIdx.x];
+      int ty = threadIdx.x;
+      asm volatile("" : "+v"(ty));
+      const Lane La = lane_state(ty);
+      const uint64_t gida = La.gid;
+      T* __restrict__ ua = La.u;
+#else
+      const uint64_t gida = gid;
+      T* __restrict__ ua = u;
+#endif
+      if (pcn_accept<T>(phu, phv, s.seed, gida, step)) {
 #pragma unroll
-        for (int j = 0; j < M; ++j) u[j] = vpark[j][threadIdx.x];
+        for (int j = 0; j < M; ++j) ua[j] = vpark[j][threadIdx.x];
         phu = phv;
         ++nacc;
       }
@@ -242,15 +287,15 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) 
       for (int j = 0; j < M; ++j) so[j] = u[j];
     }
   }
-  if (sub == 0) {
-    phi[chain] = phu;
-    if (s.accepts) s.accepts[chain] += nacc;
-    if (s.calls) s.calls[chain] += ncalls;
+  if (L0.sub == 0) {
+    phi[L0.chain] = phu;
+    if (s.accepts) s.accepts[L0.chain] += nacc;
+    if (s.calls) s.calls[L0.chain] += ncalls;
   }
   if (s.sample_out && s.sample_every == 0) {
-    T* so = (T*)s.sample_out + chain * s.sample_stride + c0;
+    T* so = (T*)s.sample_out + L0.chain * s.sample_stride + L0.c0;
 #pragma unroll
-    for (int j = 0; j < M; ++j) so[j] = u[j];
+    for (int j = 0; j < M; ++j) so[j] = L0.u[j];
   }
 }
 
@@ -357,15 +402,16 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
     // one bit per slot: the slot's lane sub == 0, at bit slot*LPC
     SpecRound rd;
     T phf;
-    unsigned long long accm = 0, okm = 0;  // G <= 64: the chain's bits
+    unsigned long long accm = 0, path = 0;  // G <= 64: the chain's bits, one per slot
     const SpecNode* tree = kSpecTrees.nd[tb];
     if (G <= 64) {
-      accm = (__ballot(acc && sub == 0) >> gbase) & gmask;
-      okm = (__ballot(ok && sub == 0) >> gbase) & gmask;
-      const int kids = spec_pack_children(nd);
-      rd = spec_walk(
-          S, left, [&](int n) { return spec_step_packed(__shfl(kids, gbase + n * LPC, 64), n, LPC, accm, okm); },
-          [](int, int) {});
+      // the walk resolved in parallel (spec_on_path): every lane tests its own
+      // node against the slots' decisions, a ballot gathers the path -- no
+      // cross-lane read inside a data-dependent loop
+      accm = spec_slot_bits((__ballot(acc && sub == 0) >> gbase) & gmask, S, LPC);
+      const unsigned long long okm = spec_slot_bits((__ballot(ok && sub == 0) >> gbase) & gmask, S, LPC);
+      path = spec_slot_bits((__ballot(spec_on_path(tb, slot, accm, act) && sub == 0) >> gbase) & gmask, S, LPC);
+      rd = spec_path_round(path, accm, okm);
       phf = __shfl(phv, gbase + (rd.win >= 0 ? rd.win : 0) * LPC, 64);
     } else {
       const unsigned long long ab = __ballot(acc && sub == 0), ob = __ballot(ok && sub == 0);
@@ -388,25 +434,29 @@ __global__ __launch_bounds__(kL96Block) void l96_spec_kernel(const ipmc_model m,
       const bool sums = s.sum_u != nullptr;
       RoundSums<M> rsum(sums ? s.sum_u + chain * D + c0 : nullptr,
                         (sums && s.sum_u2) ? s.sum_u2 + chain * D + c0 : nullptr, sums ? M : 0);
-      spec_replay(
-          rd.used,
-          [&](int n) {
-            if (G <= 64) return spec_step_bits(tree, n, LPC, accm, okm);
-            const int bit = n * LPC;
-            return spec_step_bits(tree, n, 0, wmask[0][bit >> 6] >> (bit & 63), wmask[1][bit >> 6] >> (bit & 63));
-          },
-          [&](int q, int la) {
-            if (sums) {
+      auto visit = [&](int q, int la) {
+        if (sums) {
 #pragma unroll
-              for (int j = 0; j < M; ++j) rsum.add(j, la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j]);
-            }
-            if (s.sample_every > 0 && clk.next == st + q) {
-              const int64_t sl = clk.take(clk.next);
-              T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
+          for (int j = 0; j < M; ++j) rsum.add(j, la >= 0 ? (double)vpark[j][lane0 + la * LPC] : (double)ur[j]);
+        }
+        if (s.sample_every > 0 && clk.next == st + q) {
+          const int64_t sl = clk.take(clk.next);
+          T* so = (T*)s.sample_out + chain * s.sample_stride + sl * s.sample_step_stride + c0;
 #pragma unroll
-              for (int j = 0; j < M; ++j) so[j] = la >= 0 ? vpark[j][lane0 + la * LPC] : ur[j];
-            }
-          });
+          for (int j = 0; j < M; ++j) so[j] = la >= 0 ? vpark[j][lane0 + la * LPC] : ur[j];
+        }
+      };
+      if (G <= 64) {
+        spec_path_replay(path, accm, visit);
+      } else {
+        spec_replay(
+            rd.used,
+            [&](int n) {
+              const int bit = n * LPC;
+              return spec_step_bits(tree, n, 0, wmask[0][bit >> 6] >> (bit & 63), wmask[1][bit >> 6] >> (bit & 63));
+            },
+            visit);
+      }
       if (sums) rsum.store();
     }
     if (rd.win >= 0) {

@@ -27,10 +27,27 @@ constexpr int kTsBlock = 256;
 
 // SPL 3 and 6 are compiled for K = 6 (the reference's K=6 J=4 study,
 // lorenz_mcmc.py:87-88): lanes per chain fixed at 2 (DPP halos) and 1 (none).
+// (A ring of K/3 lanes for K = 36, 5 chains = 60 live lanes per wave instead of
+// 54, measured slower: f64 needs one wave and AGPR spills at 3 x 11 values per
+// RK array, 0.94 vs 1.11 M pCN steps/s; fp32 1.53 vs 1.69 M;
+// profiles/r5/ts36_layouts.jsonl.)
 template <int SPL>
 constexpr int ts_fixed_lanes() {
   return SPL == 3 ? 2 : (SPL == 6 ? 1 : 0);
 }
+// the (SPL, J) pairs a kernel is compiled for
+template <int SPL, int J>
+constexpr bool ts_compiled() {
+  return SPL == 1 || (SPL == 2 && J <= 10) || (SPL > 2 && J <= 4);
+}
+
+// The slow ring's halos (K > 32, two slow variables per lane) through LDS --
+// one row per lane written once per stage, three neighbour reads -- instead of
+// three ds_bpermute: 1-1.6 % faster on K=36 J=10 in f64 and fp32, four
+// interleaved A/Bs (profiles/r5/ts36_layouts.jsonl); 0 for the permute form.
+#ifndef IPMC_TS_LDS_HALO
+#define IPMC_TS_LDS_HALO 1
+#endif
 
 // Occupancy target (waves per SIMD) for the sweep kernel: 4 RK4 arrays of
 // 1 + J values per lane plus the chain state.
@@ -177,9 +194,21 @@ __device__ __forceinline__ void ts_halo(const T (&Xo)[SPL], const TsCtx& c, T& p
   } else {
     const int L = c.K / SPL;
     const int prev = c.base + (c.sub + L - 1) % L, next = c.base + (c.sub + 1) % L;
+#if IPMC_TS_LDS_HALO
+    __shared__ T ring[kTsBlock][SPL];  // the wave's slow variables, one row per lane
+    const int w0 = threadIdx.x & ~63;
+#pragma unroll
+    for (int a = 0; a < SPL; ++a) ring[threadIdx.x][a] = Xo[a];
+    wave_sync_lds();
+    p1 = ring[w0 + prev][SPL - 1];
+    p2 = ring[w0 + prev][SPL - 2];
+    n0 = ring[w0 + next][0];
+    wave_sync_lds();  // read before the next stage rewrites the ring
+#else
     p1 = shfl(Xo[SPL - 1], prev);
     p2 = shfl(Xo[SPL - 2], prev);
     n0 = shfl(Xo[0], next);
+#endif
   }
 }
 
@@ -492,6 +521,7 @@ __device__ T ts_phi(const ipmc_model& m, const T (&v)[3], const TsCtx& c, int kq
 template <typename T, int J, bool FM, int SPL>
 __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep_kernel(const ipmc_model m,
                                                                                       const ipmc_sweep s, int S) {
+  __shared__ T vpk[3][kTsBlock];  // the proposals, for the recorded states of a round
   const int lane = threadIdx.x & 63;
   const int K = m.dim, L = K / SPL, G = S * L;
   const int cpw = 64 / G;
@@ -568,31 +598,35 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
     // its origin node's proposal (whose Φ that slot's lanes hold)
     const T pho = __shfl(phv, ol, 64);
     if (ok) acc = (double)((nd.orig < 0 ? phu : pho) - phv) > lr;
-    // one bit per slot (its first lane, at bit slot*L of the chain's lanes)
-    const unsigned long long accm = (__ballot(acc && c.sub == 0) >> cbase) & gmask;
-    const unsigned long long okm = (__ballot(ok && c.sub == 0) >> cbase) & gmask;
-    const int kids = spec_pack_children(nd);
-    const SpecRound rd = spec_walk(
-        S, left, [&](int n) { return spec_step_packed(__shfl(kids, cbase + n * L, 64), n, L, accm, okm); },
-        [](int, int) {});
+    // one bit per slot (its first lane, at bit slot*L of the chain's lanes); the
+    // walk resolved in parallel (spec_on_path, as ipmc_l96.hpp): no cross-lane
+    // read inside a data-dependent loop
+    const unsigned long long accm = spec_slot_bits((__ballot(acc && c.sub == 0) >> cbase) & gmask, S, L);
+    const unsigned long long okm = spec_slot_bits((__ballot(ok && c.sub == 0) >> cbase) & gmask, S, L);
+    const unsigned long long path =
+        spec_slot_bits((__ballot(spec_on_path(tb, slot, accm, act) && c.sub == 0) >> cbase) & gmask, S, L);
+    const SpecRound rd = spec_path_round(path, accm, okm);
     const int wl = cbase + (rd.win >= 0 ? rd.win : 0) * L;  // the new state's slot, first lane
     T vf[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) vf[j] = __shfl(v[j], wl, 64);
     const T phf = __shfl(phv, wl, 64);
     if (s.sum_u || s.sample_every > 0) {  // uniform per chain (only lane r == 0 keeps the clock)
-      // the states after each settled step, in step order: the same walk again,
-      // gathered by every lane of the chain (uniform per chain), written by lane r == 0
+      // the states after each settled step, in step order: the path again, the
+      // proposals read from the LDS park, written by lane r == 0
       const bool sums = s.sum_u && r == 0;
       RoundSums<3> rsum(sums ? s.sum_u + chain * 3 : nullptr, (sums && s.sum_u2) ? s.sum_u2 + chain * 3 : nullptr,
                         sums ? 3 : 0);
-      const SpecNode* tree = kSpecTrees.nd[tb];
-      spec_replay(
-          rd.used, [&](int n) { return spec_step_bits(tree, n, L, accm, okm); },
+#pragma unroll
+      for (int j = 0; j < 3; ++j) vpk[j][threadIdx.x] = v[j];
+      wave_sync_lds();
+      const int t0 = (threadIdx.x & ~63) + cbase;  // the chain's first thread in the block
+      spec_path_replay(
+          path, accm,
           [&](int q, int la) {
             T vq[3];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) vq[j] = __shfl(v[j], cbase + (la >= 0 ? la : 0) * L, 64);
+            for (int j = 0; j < 3; ++j) vq[j] = vpk[j][t0 + (la >= 0 ? la : 0) * L];
             if (r == 0) {
               if (sums) {
 #pragma unroll
@@ -607,6 +641,7 @@ __global__ __launch_bounds__(kTsBlock, (ts_waves<T, J, SPL>())) void l96ts_sweep
             }
           });
       if (sums) rsum.store();
+      wave_sync_lds();  // the park is rewritten next round
     }
     if (rd.win >= 0) {
 #pragma unroll
@@ -707,7 +742,7 @@ static int ts_sweep_t(const ipmc_model& m, const ipmc_sweep& s, hipStream_t st) 
   switch (m.fast_per_slow) {
 #define IPMC_J(J)                                                                                                  \
   case J:                                                                                                          \
-    if constexpr (SPL == 1 || (SPL == 2 && J <= 10) || (SPL > 2 && J <= 4)) {                                     \
+    if constexpr (ts_compiled<SPL, J>()) {                                     \
       hipLaunchKernelGGL((l96ts_sweep_kernel<T, J, FM, SPL>), dim3((unsigned)blocks), dim3(kTsBlock), 0, st, m, s, \
                          S);                                                                                       \
       return check_launch("l96ts_sweep_kernel");                                                                   \
@@ -727,7 +762,7 @@ static int ts_eval_t(const ipmc_model& m, int64_t n, const void* u, const void* 
   switch (m.fast_per_slow) {
 #define IPMC_J(J)                                                                                                 \
   case J:                                                                                                         \
-    if constexpr (SPL == 1 || (SPL == 2 && J <= 10) || (SPL > 2 && J <= 4)) {                                    \
+    if constexpr (ts_compiled<SPL, J>()) {                                    \
       if (phi)                                                                                                    \
         hipLaunchKernelGGL((l96ts_eval_kernel<T, J, FM, SPL, true>), dim3((unsigned)blocks), dim3(kTsBlock), 0,   \
                            st, m, n, (const T*)u, (const T*)y, (const T*)ginv, (T*)out);                          \

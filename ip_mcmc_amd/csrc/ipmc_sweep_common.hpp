@@ -320,6 +320,14 @@ __device__ __forceinline__ SpecRound spec_path_round(unsigned long long path, un
   r.win = pa ? 63 - __builtin_clzll(pa) : -1;  // the deepest accepted node of the path
   return r;
 }
+// One bit per slot (bit n = slot n) from a ballot holding slot n's bit at
+// n*L (L lanes per slot, S slots, S*L <= 64).
+__device__ __forceinline__ unsigned long long spec_slot_bits(unsigned long long m, int S, int L) {
+  if (L == 1) return m;
+  unsigned long long b = 0;
+  for (int n = 0; n < S; ++n) b |= ((m >> (n * L)) & 1ull) << n;
+  return b;
+}
 // visit(q, la) over the path's steps, as spec_walk's
 template <class Visit>
 __device__ __forceinline__ void spec_path_replay(unsigned long long path, unsigned long long acc, Visit&& visit) {

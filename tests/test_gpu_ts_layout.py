@@ -1,7 +1,8 @@
 """Two-scale Lorenz-96 lane layouts: one or two slow variables per lane
-(lanes_per_chain = K or K/2) and, for K = 6 with J <= 4, three (2 lanes, DPP
-halos) or all six (1 lane), with and without speculative slots, equal the
-oracle bit for bit (G, Φ and sweeps)."""
+(lanes_per_chain = K or K/2; for K > 32 the ring's halos go through LDS) and,
+for K = 6 with J <= 4, three (2 lanes, DPP halos) or all six (1 lane), with
+and without speculative slots, equal the oracle bit for bit (G, Φ and
+sweeps)."""
 import numpy as np
 import pytest
 
@@ -18,7 +19,7 @@ def dev_ts():
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-@pytest.mark.parametrize("K,J", [(2, 4), (6, 4), (4, 10), (36, 10), (40, 2), (64, 1), (8, 8)])
+@pytest.mark.parametrize("K,J", [(2, 4), (6, 4), (4, 10), (36, 10), (40, 2), (64, 1), (8, 8), (48, 8)])
 def test_ts_two_slow_per_lane_bit_exact(dev_ts, orc, dtype, K, J):
     from ip_mcmc_amd import TwoScaleLorenz96Operator
 

@@ -1,7 +1,10 @@
 """Debug: which speculative ts / Burgers sweep sums differ from the oracle.
 
   [IPMC_LIB_PATH=variant] python tools/probes/spec_tree_debug.py [case-prefix ...]
-  (e.g. `bur128` with the IPMC_PROBE_WALK_SHFL variant: round 4's failing form)
+  (round 5 ran `bur128` against variant builds whose walk read the proposals by
+  __shfl -- from every lane of the chain: correct, profiles/r5/walk_shfl_all_lanes.txt;
+  under the first lane's branch, the source lanes inactive: wrong sums,
+  profiles/r5/walk_shfl_first_lane.txt)
 """
 import os
 import sys

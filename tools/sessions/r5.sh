@@ -29,6 +29,64 @@ case "$1" in
           python tools/probes/arith_kernel_probe.py w2fma >> $O/arith_waves_ab.jsonl || exit $?
     done
     ;;
+  s2)
+    # the whole GPU suite on the tree (REFERENCE arith at two waves, the K/3
+    # two-scale ring, the paired-stream tests), the walk probe with the read
+    # under the first lane's branch, the two-scale K=36 layout / halo A/B
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_s2.log 2>&1
+    IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/walkshfl2/libipmc.so timeout -k 10 300 \
+        python tools/probes/spec_tree_debug.py bur128 > $O/walk_shfl_first_lane.txt 2>&1 &&
+    for i in 1 2; do
+      timeout -k 10 300 python tools/config_bench.py ts36 ts36:12 >> $O/ts36_layouts.jsonl &&
+      IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/tslds/libipmc.so timeout -k 10 300 \
+          python tools/config_bench.py ts36 ts36:12 | sed 's/^{/{"variant": "lds_halo", /' >> $O/ts36_layouts.jsonl || exit $?
+    done
+    ;;
+  s3)
+    # in-wave speculative rounds resolved in parallel (L96, Burgers, two-scale):
+    # the whole suite, then the speculation rows and the reference studies
+    # against the walk build (variants/prevwalk = the previous commit)
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_s3.log 2>&1
+    R="l96mx1@256 l96mx64@256 l96mx1024@256 l96x1@256 l96x64@256 cfg2@16384"
+    for i in 1 2; do
+      for lib in "" ip_mcmc_amd/lib/variants/prevwalk/libipmc.so; do
+        IPMC_LIB_PATH=$lib timeout -k 10 300 python tools/config_bench.py $R | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin]" \
+          >> $O/walk_ab_rows.jsonl &&
+        IPMC_LIB_PATH=$lib timeout -k 10 200 python tools/probes/burgers_spec_probe.py 1024 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin if l.startswith('{')]" \
+          >> $O/walk_ab_burgers.jsonl &&
+        IPMC_LIB_PATH=$lib timeout -k 10 200 python tools/probes/burgers_spec_probe.py 1 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin if l.startswith('{')]" \
+          >> $O/walk_ab_burgers.jsonl &&
+        IPMC_LIB_PATH=$lib timeout -k 10 300 python examples/lorenz_thesis.py 1024 | \
+          python -c "import json,sys;[print(json.dumps(dict(json.loads(l),lib='${lib:-product}'))) for l in sys.stdin if l.startswith('{')]" \
+          >> $O/walk_ab_lorenz.jsonl || exit 1
+      done
+    done
+    ;;
+  s4)
+    # the fp64 Lorenz-96 sweep with its lane state parked in LDS across G at
+    # two waves per SIMD (variants/park) against the product (one wave for
+    # FMA), FMA and REFERENCE arith, interleaved three times; PMC traffic of both
+    V=ip_mcmc_amd/lib/variants/park/libipmc.so
+    B="python bench.py --kernel-only --no-cpu --steps 5 --warmup 1"
+    SQC="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+    for i in 1 2 3; do
+      timeout -k 10 120 python tools/probes/arith_kernel_probe.py product >> $O/park_ab.jsonl &&
+      IPMC_LIB_PATH=$V timeout -k 10 120 python tools/probes/arith_kernel_probe.py park >> $O/park_ab.jsonl || exit 1
+    done &&
+    for lib in product park; do
+      L=""; [ $lib = park ] && L=$V
+      IPMC_LIB_PATH=$L timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+          -d $O/pmc_$lib/fetch -o run -- $B > /dev/null &&
+      IPMC_LIB_PATH=$L timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+          -d $O/pmc_$lib/write -o run -- $B > /dev/null &&
+      IPMC_LIB_PATH=$L timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv \
+          -d $O/pmc_$lib/sq -o run -- $B > /dev/null &&
+      python tools/pmc_summarize.py $O/pmc_$lib f64 65536 $O/pmc_l96_f64_$lib.json 6 || exit 1
+    done
+    ;;
   *)
     echo "unknown session $1"; exit 2
     ;;
