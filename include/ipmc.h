@@ -30,6 +30,8 @@
  *                                     lorenz_mcmc.py:17-40
  *   MCMCSampler.autocorr              sampler.py:43-54        ipmc_autocorr
  *   len_burn_in                       burgers/utilities.py:134-167  ipmc_burn_in
+ *   np.mean over the samples          sampler.py:20-28 callers ipmc_ordered_sum (the many-chain posterior
+ *                                     (e.g. stuart_examples.py)  mean's chain-ordered sum, on the device)
  *
  * The reference has no FFI of its own (it is duck-typed Python); these entry
  * points are what a ctypes binding of its plugin API binds.
@@ -58,7 +60,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 11
+#define IPMC_ABI_VERSION 12
 
 typedef enum {
   IPMC_OK = 0,
@@ -246,6 +248,13 @@ int ipmc_autocorr(const void* x, int32_t dtype, int64_t n_series, int64_t len, i
 int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars, int64_t len, int64_t stride_chain,
                  int64_t stride_var, int64_t stride_t, int32_t window, double threshold, uint32_t* flags_scratch,
                  int64_t* out, void* stream);
+
+/* (ABI 12) acc[j] = (((acc[j] + rows[0][j]/div) + rows[1][j]/div) + ...) for j < k over the n_rows rows
+   (row r at rows + r*row_stride doubles), strictly in row order -- the chain-ordered sum of the many-chain
+   posterior mean (shard.ordered_sum_sharded), equal bit for bit to ipmc_host_ordered_sum (ipmc_host.h);
+   div == 1 adds the rows as they are.  Device pointers; acc [k] in/out. */
+int ipmc_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div, double* acc,
+                     void* stream);
 
 /* Lorenz-96 layout of a ONE-step launch (no speculation) when lanes_per_chain = chains_per_lane = 0:
    returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout.

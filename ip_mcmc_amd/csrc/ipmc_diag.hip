@@ -259,9 +259,49 @@ __global__ void burn_in_search_kernel(int64_t n_chains, int64_t len, int w, cons
   out[c] = res;
 }
 
+// The chain-ordered column sums behind the many-chain posterior mean
+// (shard.ordered_sum_sharded): acc[j] = (((acc[j] + x_0j/div) + x_1j/div) + ...)
+// strictly in row order, the additions of ipmc_host_ordered_sum (same IEEE
+// operations, -ffp-contract=off: the same bits).  One lane per column walks the
+// rows: a dependent chain of adds, its loads issued ahead by the unrolled loop
+// (consecutive lanes read consecutive columns of a row: coalesced).
+constexpr int kOsBlock = 64;
+
+__global__ __launch_bounds__(kOsBlock) void ordered_sum_kernel(const double* __restrict__ x, int64_t n_rows, int64_t k,
+                                                              int64_t stride, double div, double* __restrict__ acc) {
+  const int64_t j = (int64_t)blockIdx.x * kOsBlock + threadIdx.x;
+  if (j >= k) return;
+  const double* p = x + j;
+  double a = acc[j];
+  if (div == 1.0) {
+#pragma unroll 16
+    for (int64_t r = 0; r < n_rows; ++r) a = a + p[r * stride];
+  } else {
+#pragma unroll 16
+    for (int64_t r = 0; r < n_rows; ++r) a = a + p[r * stride] / div;
+  }
+  acc[j] = a;
+}
+
 }  // namespace ipmc
 
 using namespace ipmc;
+
+extern "C" int ipmc_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div,
+                                double* acc, void* stream) {
+  if (n_rows < 0 || k < 0 || row_stride < k) {
+    set_error("ipmc_ordered_sum: bad shape (n_rows, k >= 0, row_stride >= k)");
+    return IPMC_ERR_INVALID;
+  }
+  if (n_rows == 0 || k == 0) return IPMC_OK;
+  if (!rows || !acc) {
+    set_error("ipmc_ordered_sum: NULL pointer");
+    return IPMC_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((k + kOsBlock - 1) / kOsBlock)), dim3(kOsBlock), 0,
+                     (hipStream_t)stream, rows, n_rows, k, row_stride, div, acc);
+  return check_launch("ordered_sum_kernel");
+}
 
 extern "C" int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars, int64_t len,
                             int64_t stride_chain, int64_t stride_var, int64_t stride_t, int32_t window,

@@ -132,29 +132,30 @@ __device__ __forceinline__ V l96_potential(const V (&v)[M], const S* __restrict_
 // RK loop keeps 5 arrays of M values live (x, F, time-average, k-sum, stage;
 // l96_stage consumes each rate as it is computed), the proposal / accept stage
 // ~40 registers of addressing / RNG / loop state around it.  The target is
-// sized for 6 arrays (fp64 M = 20: one wave, where the FMA kernel takes 271
-// registers -- 256 VGPRs and 15 AGPRs -- without scratch; it issues in every
-// VALU slot at one wave per SIMD).
+// sized for 6 arrays (fp64 M = 17-20: see below).
 // (fp32 one chain per lane group: the compiler's SLP packing needs ~96; every
 // variant gets at least 104 registers, i.e. at most 4 waves, since the
 // proposal / accept stage spills below that: 20-56 B per lane at 5 waves for
 // M <= 5, e.g. d=40 at 8 lanes per chain.)
-// REFERENCE arith in fp64 at 17-20 components per lane (the headline's d=40 on
-// 2 lanes): held to two waves.  Left free (one wave), the compiler took 258
-// registers, one wave per SIMD; at two it spills 12 B per lane outside the RK
-// loop and the headline kernel runs 5.24 -> 4.89 ms (12.5 -> 13.4 M pCN
-// steps/s; profiles/r5/arith_waves_ab.jsonl).  The FMA kernel gains 2 % the
-// same way but spills 80 B per lane, as much HBM traffic as the compulsory
-// bytes: it stays at one wave.
-#ifndef IPMC_L96_PARK  // A/B: the sequential sweep's lane state parked in LDS across G, fp64 M 17-20 at two waves
-#define IPMC_L96_PARK 0
+// fp64 at 17-20 components per lane (the headline's d=40 on 2 lanes): held to
+// two waves.  Left free, the compiler took 258 (REFERENCE) / 271 (FMA)
+// registers, one wave per SIMD.  At two waves it spilled what lives across G
+// (the lane's chain index and addresses, Φ(u): 12 / 80 B per lane); with
+// IPMC_L96_PARK the sequential sweep recomputes the lane state from the
+// thread index after G and parks Φ(u) in LDS, so nothing spills: the headline
+// kernel 3.20 -> 3.13 ms (FMA; profiles/r5/park_ab.jsonl), REFERENCE arith
+// 5.24 -> 4.89 ms (profiles/r5/arith_waves_ab.jsonl).
+#ifndef IPMC_L96_PARK  // 0: the lane state kept in registers across G (A/B)
+#define IPMC_L96_PARK 1
 #endif
-template <typename T, int M, bool FM = true>
+// (LPC >= 8 stages the misfit through another M x 256 LDS array: two blocks of
+// it do not fit the CU's 160 KiB, so those layouts stay at one wave.)
+template <typename T, int M, bool FM = true, int LPC = 1>
 constexpr int l96_waves_per_simd() {
 #ifdef IPMC_L96_WAVES  // occupancy experiments (tools/)
   return IPMC_L96_WAVES;
 #endif
-  if constexpr ((!FM || IPMC_L96_PARK) && sizeof(T) == 8 && M >= 17 && M <= 20) return 2;
+  if constexpr ((!FM || IPMC_L96_PARK) && sizeof(T) == 8 && M >= 17 && M <= 20 && LPC < 8) return 2;
   constexpr int want = 6 * M * (int)(sizeof(T) / 4) + (sizeof(T) == 8 ? 40 : 96);
   constexpr int regs = want < 104 ? 104 : want;
   constexpr int w = 512 / regs;
@@ -179,7 +180,7 @@ constexpr int l96_pk_waves_per_simd() {
 
 // n_steps pCN steps per launch; u / Φ(u) / accept counts updated in place.
 template <typename T, int D, int LPC, bool FM>
-__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) void l96_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
+__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM, LPC>())) void l96_sweep_kernel(const ipmc_model m, const ipmc_sweep s) {
   constexpr int M = D / LPC;
   constexpr bool IL = (LPC == 8);  // interleaved groups of 8 (group_vlane)
   __shared__ T vpark[M][kL96Block];  // proposal parked in LDS while G runs
@@ -287,15 +288,22 @@ __global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) 
       for (int j = 0; j < M; ++j) so[j] = u[j];
     }
   }
-  if (L0.sub == 0) {
-    phi[L0.chain] = phu;
-    if (s.accepts) s.accepts[L0.chain] += nacc;
-    if (s.calls) s.calls[L0.chain] += ncalls;
+#if IPMC_L96_PARK
+  int te = threadIdx.x;
+  asm volatile("" : "+v"(te));
+  const Lane Le = lane_state(te);
+#else
+  const Lane& Le = L0;
+#endif
+  if (Le.sub == 0) {
+    phi[Le.chain] = phu;
+    if (s.accepts) s.accepts[Le.chain] += nacc;
+    if (s.calls) s.calls[Le.chain] += ncalls;
   }
   if (s.sample_out && s.sample_every == 0) {
-    T* so = (T*)s.sample_out + L0.chain * s.sample_stride + L0.c0;
+    T* so = (T*)s.sample_out + Le.chain * s.sample_stride + Le.c0;
 #pragma unroll
-    for (int j = 0; j < M; ++j) so[j] = L0.u[j];
+    for (int j = 0; j < M; ++j) so[j] = Le.u[j];
   }
 }
 
@@ -626,7 +634,7 @@ __global__ __launch_bounds__(kL96Block, (l96_pk_waves_per_simd<D / LPC>())) void
 
 // G(u) or Φ(u) for n parameter vectors (no proposal): out = g [n, D] or phi [n].
 template <typename T, int D, int LPC, bool FM, bool PHI>
-__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM>())) void l96_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
+__global__ __launch_bounds__(kL96Block, (l96_waves_per_simd<T, D / LPC, FM, LPC>())) void l96_eval_kernel(const ipmc_model m, int64_t n, const T* __restrict__ uin,
                                                               const T* __restrict__ yin,
                                                               const T* __restrict__ ginvin, T* __restrict__ out) {
   constexpr int M = D / LPC;

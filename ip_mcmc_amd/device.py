@@ -74,6 +74,20 @@ def copy_rows_d2h(dst, dst_pitch, src, src_pitch, width, rows, stream):
     call("ipmc_copy_rows_d2h", dst, dst_pitch, src, src_pitch, width, rows, stream)
 
 
+def ordered_sum(rows, acc, div=1.0):
+    """acc (device f64 [k], in place) + rows[0]/div + rows[1]/div + ... strictly
+    in row order on the device (ipmc_ordered_sum, the current stream): the bits
+    of the host library's ipmc_host_ordered_sum.  rows: device f64 [n, k] with
+    unit column stride."""
+    if rows.dtype != torch.float64 or acc.dtype != torch.float64 or rows.dim() != 2 or rows.stride(1) != 1:
+        raise ValueError("ordered_sum needs f64 rows [n, k] with contiguous columns and an f64 acc")
+    if acc.shape != (rows.shape[1],) or not acc.is_contiguous() or acc.device != rows.device:
+        raise ValueError("ordered_sum: acc must be a contiguous [k] tensor on the rows' device")
+    call("ipmc_ordered_sum", rows.data_ptr(), rows.shape[0], rows.shape[1], rows.stride(0), float(div),
+         acc.data_ptr(), stream_handle(rows.device))
+    return acc
+
+
 def normals(seed, chain_offset, n_chains, step, k, dtype=None, device=None):
     device = resolve_device(device)
     td = torch_dtype(dtype)

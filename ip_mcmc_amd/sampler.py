@@ -149,6 +149,11 @@ class MCMCSampler:
         # state of the last run (device tensors), for inspection / continuation
         self.state = None
         self.last_run_seconds = None
+        # keep_device_sums: a keep="moments" device run leaves its (sum_u,
+        # sum_u2) device tensors in last_device_sums (shard.run_sharded sums
+        # them on the device for the posterior mean); off by default
+        self.keep_device_sums = False
+        self.last_device_sums = None
         # "device" (fused kernels), "host" / "host-generic" (hostloop.py) for the last run
         self.last_path = None
         self.last_run_timing = None
@@ -169,6 +174,7 @@ class MCMCSampler:
         if keep not in ("samples", "moments", "last"):
             raise ValueError("keep must be 'samples', 'moments' or 'last'")
         t_entry = time.perf_counter()
+        self.last_device_sums = None
         try:
             plan = _Plan(self.proposer, self.accepter)
         except UnsupportedOnDevice as e:
@@ -477,6 +483,7 @@ class MCMCSampler:
                 return sink.close()
             out = host_out.numpy()  # shares the page-locked buffer (kept alive by the array)
             return out[0] if single else out
+        self.last_device_sums = sums if (keep == "moments" and self.keep_device_sums) else None
         if keep == "moments":
             n_post = n_samples * sample_interval
             res = {"sum_u": sums_host[0].numpy(), "sum_u2": sums_host[1].numpy(), "n": n_post}

@@ -6,8 +6,10 @@ contiguous block of global chain ids and passes its first id as
 so every chain's trajectory is bitwise identical for any P.  The only
 collective is the final gather of per-chain results to every rank
 (``torch.distributed.all_gather_into_tensor``; backend "nccl" = RCCL over
-xGMI on MI355X, "gloo" on CPU), followed by a host reduction in fixed global
-chain order, so posterior means are also bitwise independent of P.
+xGMI on MI355X, "gloo" on CPU) and a reduction in fixed global chain order
+(rank-sequential, on the device when the sums are; ipmc_ordered_sum /
+ipmc_host_ordered_sum, the same bits), so posterior means are also bitwise
+independent of P.
 """
 import os
 
@@ -70,7 +72,12 @@ def ordered_sum_sharded(local, group=None, div=1.0):
     continues rank r-1's running sum (one small message per rank boundary,
     send/recv), and the last rank's total is broadcast to every rank.
     Bit-identical to ordered_mean's sum over the gathered rows, without
-    gathering them (config 5's per-chain sums are 4 GB)."""
+    gathering them (config 5's per-chain sums are 4 GB).  `local` on the
+    device (a CUDA tensor, e.g. MCMCSampler's sums) keeps every hop on the
+    device: the sum is ipmc_ordered_sum (the same bits), and only the k totals
+    move -- no host round trip per rank."""
+    if isinstance(local, torch.Tensor) and local.is_cuda:
+        return _ordered_sum_sharded_device(local, group, div)
     rank, world = world_info(group)
     a = np.asarray(local, dtype=np.float64)
     acc = np.zeros(a.shape[1:], dtype=np.float64)
@@ -88,6 +95,30 @@ def ordered_sum_sharded(local, group=None, div=1.0):
     t = torch.from_numpy(np.ascontiguousarray(acc)).to(dev)
     dist.broadcast(t, src=glob(world - 1), group=group)
     return t.cpu().numpy()
+
+
+def _ordered_sum_sharded_device(rows, group, div):
+    from . import device as D
+
+    rank, world = world_info(group)
+    rows = rows.reshape(rows.shape[0], -1)
+    acc = torch.zeros(rows.shape[1], dtype=torch.float64, device=rows.device)
+    if world > 1:
+        comm = _comm_device(group)
+        glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+        if rank > 0:
+            t = torch.empty_like(acc, device=comm)
+            dist.recv(t, src=glob(rank - 1), group=group)
+            acc.copy_(t)
+    if rows.shape[0]:
+        D.ordered_sum(rows, acc, div)
+    if world > 1:
+        if rank < world - 1:
+            dist.send(acc.to(comm), dst=glob(rank + 1), group=group)
+        t = acc.to(comm)
+        dist.broadcast(t, src=glob(world - 1), group=group)
+        acc = t
+    return acc.cpu().numpy()
 
 
 def world_info(group=None):
@@ -155,6 +186,9 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     sampler = make_sampler(chain_offset=lo)
     if sampler.chain_offset != lo:
         raise ValueError(f"make_sampler must build the sampler with chain_offset={lo}, got {sampler.chain_offset}")
+    # gather="mean": the posterior mean's ordered sum runs on the device sums
+    # the sweeps left (MCMCSampler.last_device_sums) when the run was a device run
+    sampler.keep_device_sums = gather == "mean"
     local_u0 = np.asarray(u_0[lo:hi], dtype=np.float64)
     sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
     t0 = time.perf_counter()
@@ -168,13 +202,19 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
             np.asarray(st.accepts, dtype=np.float64).reshape(hi - lo, 1)]  # counts < 2^53: exact
     if gather == "mean":
         t1 = time.perf_counter()
-        small = np.concatenate(cols[1:], axis=1)
         if world > 1:
+            small = np.concatenate(cols[1:], axis=1)
             small = gather_chains(torch.from_numpy(np.ascontiguousarray(small)).to(_comm_device(group)), n_total,
                                   group).cpu().numpy()
+            phi_all, acc_all = small[:, 0], small[:, 1].astype(np.int64)
+        else:  # one rank: this process's arrays are the result
+            phi_all, acc_all = cols[1][:, 0], np.asarray(st.accepts, dtype=np.int64)
         n = max(1, res["n"])
-        mean = ordered_sum_sharded(res["sum_u"].reshape(hi - lo, k), group) / (float(n) * n_total)
-        return {"u": cols[0], "phi": small[:, 0], "accepts": small[:, 1].astype(np.int64), "sum_u": res["sum_u"],
+        dsum = getattr(sampler, "last_device_sums", None)
+        rows = dsum[0] if dsum is not None else res["sum_u"].reshape(hi - lo, k)
+        mean = ordered_sum_sharded(rows, group) / (float(n) * n_total)
+        sampler.last_device_sums = None
+        return {"u": cols[0], "phi": phi_all, "accepts": acc_all, "sum_u": res["sum_u"],
                 "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
                 "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
                 "gather_seconds": time.perf_counter() - t1}

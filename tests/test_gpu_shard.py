@@ -80,3 +80,67 @@ def test_two_rank_gpu_run_equals_one_process(tmp_path):
     assert np.array_equal(got["S"], samples.reshape(C_TOTAL, -1))
     assert np.array_equal(got["acc"], accepts)
     assert np.array_equal(got["mean"], ordered_mean(torch.from_numpy(samples.reshape(C_TOTAL, -1))))
+
+
+def test_device_ordered_sum_equals_the_host_library():
+    """ipmc_ordered_sum (the device's chain-ordered column sums) == the host
+    library's ipmc_host_ordered_sum bit for bit: mixed magnitudes, a row stride
+    wider than k, div != 1, a running acc, no rows."""
+    from ip_mcmc_amd import _hostlib
+    from ip_mcmc_amd import device as D
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(4)
+    for n, k, stride, div in ((65536, 40, 40, 1.0), (3001, 257, 300, 7.0), (5, 3, 3, 0.5), (0, 4, 4, 2.0),
+                              (1, 1, 1, 1.0)):
+        a = rng.normal(size=(n, stride)) * np.exp(rng.normal(scale=6, size=(n, 1)))
+        acc0 = rng.normal(size=k)
+        want = acc0.copy()
+        if n:
+            _hostlib.call("ipmc_host_ordered_sum", a.ctypes.data, n, k, stride, float(div), want.ctypes.data)
+        rows = torch.as_tensor(a, device=dev)[:, :k]
+        acc = torch.as_tensor(acc0, device=dev).clone()
+        D.ordered_sum(rows, acc, div)
+        assert np.array_equal(acc.cpu().numpy(), want), (n, k, stride, div)
+
+
+def _mean_worker(rank, world, port, out_path):
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import run_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="mean")
+    assert res["sampler"].last_path == "device" and res["sampler"].last_device_sums is None
+    if rank == 1:
+        np.savez(out_path, mean=res["mean"], phi=res["phi"], acc=res["accepts"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _make_sampler(chain_offset=0):
+    from ip_mcmc_amd import (ConstSteppCNProposer, EvolutionPotential, GaussianDistribution, Lorenz96Operator,
+                             MCMCSampler, pCNAccepter)
+
+    G = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=150)
+    y = G(np.zeros(K)) + 0.1 * np.random.default_rng(3).normal(size=K)
+    pot = EvolutionPotential(G, y, GaussianDistribution(np.zeros(K), 0.01 * np.eye(K)))
+    return MCMCSampler(ConstSteppCNProposer(0.1, GaussianDistribution(np.zeros(K), np.eye(K))), pCNAccepter(pot), 7,
+                       chain_offset=chain_offset)
+
+
+def test_run_sharded_mean_on_the_device_equals_the_host_mean(tmp_path):
+    """gather='mean' sums the sweeps' device sums (ipmc_ordered_sum, rank by
+    rank): one process and two ranks (gloo hops, both on cuda:0) give the host
+    ordered mean of the per-chain sums bit for bit."""
+    from ip_mcmc_amd.shard import _seq_sum, run_sharded
+
+    one = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="mean")
+    host = _seq_sum(one["sum_u"], np.zeros(K)) / (float(one["n"]) * C_TOTAL)  # the host library's sum
+    assert np.array_equal(one["mean"], host)
+    out = str(tmp_path / "m.npz")
+    mp.start_processes(_mean_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    got = np.load(out)
+    assert np.array_equal(got["mean"], one["mean"])
+    assert np.array_equal(got["phi"], one["phi"]) and np.array_equal(got["acc"], one["accepts"])

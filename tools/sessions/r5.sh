@@ -87,6 +87,14 @@ case "$1" in
       python tools/pmc_summarize.py $O/pmc_$lib f64 65536 $O/pmc_l96_f64_$lib.json 6 || exit 1
     done
     ;;
+  s5)
+    # the tree with the parked fp64 sweep at two waves, the device ordered sum
+    # (ABI 12): the whole suite, smoke, the default line
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_s5.log 2>&1
+    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s5.txt 2>&1 &&
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_s5_k20.json 2> $O/bench_s5_k20.err &&
+    timeout -k 10 600 python bench.py --no-configs --no-cpu > $O/bench_s5_k200.json 2> $O/bench_s5_k200.err
+    ;;
   *)
     echo "unknown session $1"; exit 2
     ;;
