@@ -709,6 +709,12 @@ def main():
                 "lanes_per_chain": lanes_k,
                 "chains_per_lane": cpl_k,
                 "spec_width": spec_k,
+                # the benched arithmetic against the reference's operation order (parity.*)
+                "arith_parity": None if not parity else {
+                    "paired_identical_accept_stream_frac": parity.get("paired_identical_accept_frac"),
+                    "paired_chains": parity.get(args.workload, {}).get("chains"),
+                    "paired_steps": parity.get(args.workload, {}).get("steps"),
+                    "reference_arith_value": parity.get("reference_arith_value")},
                 "parallelism": f"{total_chains} chains sharded over {world} GPU(s) ({args.scaling} scaling)",
                 "clock_settle_s": args.settle,
             },

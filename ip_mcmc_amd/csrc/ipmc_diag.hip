@@ -262,25 +262,61 @@ __global__ void burn_in_search_kernel(int64_t n_chains, int64_t len, int w, cons
 // The chain-ordered column sums behind the many-chain posterior mean
 // (shard.ordered_sum_sharded): acc[j] = (((acc[j] + x_0j/div) + x_1j/div) + ...)
 // strictly in row order, the additions of ipmc_host_ordered_sum (same IEEE
-// operations, -ffp-contract=off: the same bits).  One lane per column walks the
-// rows: a dependent chain of adds, its loads issued ahead by the unrolled loop
-// (consecutive lanes read consecutive columns of a row: coalesced).
-constexpr int kOsBlock = 64;
+// operations, -ffp-contract=off: the same bits).  The sum of a column is one
+// dependent chain of adds, so the kernel keeps that chain fed: a block owns 64
+// columns; wave 0 holds one column per lane and adds chunk c (8 192 values)
+// from LDS while waves 1-3 stream chunk c + 1 from global memory into the other
+// LDS buffer (coalesced, many loads in flight) -- one barrier per chunk.  A
+// lane walking the rows straight from global memory waits out a load latency
+// per row or per unrolled group (2.5 ms for 65 536 x 40 values on the MI355X,
+// more than the host library's one pass).
+constexpr int kOsCols = 64;     // columns per block (wave 0: one per lane)
+constexpr int kOsBuf = 8192;    // doubles per LDS buffer: 8192 / kc rows per chunk
+constexpr int kOsBlock = 256;   // wave 0 adds, waves 1-3 load
 
 __global__ __launch_bounds__(kOsBlock) void ordered_sum_kernel(const double* __restrict__ x, int64_t n_rows, int64_t k,
                                                               int64_t stride, double div, double* __restrict__ acc) {
-  const int64_t j = (int64_t)blockIdx.x * kOsBlock + threadIdx.x;
-  if (j >= k) return;
-  const double* p = x + j;
-  double a = acc[j];
-  if (div == 1.0) {
-#pragma unroll 16
-    for (int64_t r = 0; r < n_rows; ++r) a = a + p[r * stride];
-  } else {
-#pragma unroll 16
-    for (int64_t r = 0; r < n_rows; ++r) a = a + p[r * stride] / div;
+  __shared__ double buf[2][kOsBuf];
+  const int t = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * kOsCols;
+  const int kc = (int)((k - c0) < kOsCols ? (k - c0) : kOsCols);
+  const int R = kOsBuf / kc;  // rows per chunk
+  const int64_t n_chunks = (n_rows + R - 1) / R;
+  auto rows_of = [&](int64_t chunk) {
+    const int64_t left = n_rows - chunk * R;
+    return (int)(left < R ? left : R);
+  };
+  auto load = [&](int64_t chunk, int b) {  // waves 1-3: chunk -> buf[b], row-major [rows][kc]
+    const int64_t r0 = chunk * R;
+    const int n = rows_of(chunk) * kc;
+    for (int i = t - 64; i < n; i += kOsBlock - 64) {
+      const int r = i / kc, j = i - r * kc;
+      buf[b][i] = x[(r0 + r) * stride + c0 + j];
+    }
+  };
+  double a = 0.0;
+  if (t < kc) a = acc[c0 + t];
+  if (t >= 64) load(0, 0);
+  __syncthreads();
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    if (t < 64) {
+      if (t < kc) {
+        const int rows = rows_of(c);
+        const double* bb = buf[c & 1] + t;
+        if (div == 1.0) {
+#pragma unroll 8
+          for (int r = 0; r < rows; ++r) a = a + bb[r * kc];
+        } else {
+#pragma unroll 8
+          for (int r = 0; r < rows; ++r) a = a + bb[r * kc] / div;
+        }
+      }
+    } else if (c + 1 < n_chunks) {
+      load(c + 1, (int)((c + 1) & 1));
+    }
+    __syncthreads();  // chunk c consumed and chunk c + 1 in place
   }
-  acc[j] = a;
+  if (t < kc) acc[c0 + t] = a;
 }
 
 }  // namespace ipmc
@@ -298,7 +334,7 @@ extern "C" int ipmc_ordered_sum(const double* rows, int64_t n_rows, int64_t k, i
     set_error("ipmc_ordered_sum: NULL pointer");
     return IPMC_ERR_INVALID;
   }
-  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((k + kOsBlock - 1) / kOsBlock)), dim3(kOsBlock), 0,
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3((unsigned)((k + kOsCols - 1) / kOsCols)), dim3(kOsBlock), 0,
                      (hipStream_t)stream, rows, n_rows, k, row_stride, div, acc);
   return check_launch("ordered_sum_kernel");
 }

@@ -79,10 +79,14 @@ def ordered_sum(rows, acc, div=1.0):
     in row order on the device (ipmc_ordered_sum, the current stream): the bits
     of the host library's ipmc_host_ordered_sum.  rows: device f64 [n, k] with
     unit column stride."""
-    if rows.dtype != torch.float64 or acc.dtype != torch.float64 or rows.dim() != 2 or rows.stride(1) != 1:
-        raise ValueError("ordered_sum needs f64 rows [n, k] with contiguous columns and an f64 acc")
+    if rows.dtype != torch.float64 or acc.dtype != torch.float64 or rows.dim() != 2:
+        raise ValueError("ordered_sum needs f64 rows [n, k] and an f64 acc")
     if acc.shape != (rows.shape[1],) or not acc.is_contiguous() or acc.device != rows.device:
         raise ValueError("ordered_sum: acc must be a contiguous [k] tensor on the rows' device")
+    if rows.shape[0] == 0 or rows.shape[1] == 0:
+        return acc
+    if rows.stride(1) != 1:
+        raise ValueError("ordered_sum needs rows with contiguous columns")
     call("ipmc_ordered_sum", rows.data_ptr(), rows.shape[0], rows.shape[1], rows.stride(0), float(div),
          acc.data_ptr(), stream_handle(rows.device))
     return acc

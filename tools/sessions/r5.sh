@@ -95,6 +95,49 @@ case "$1" in
     timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_s5_k20.json 2> $O/bench_s5_k20.err &&
     timeout -k 10 600 python bench.py --no-configs --no-cpu > $O/bench_s5_k200.json 2> $O/bench_s5_k200.err
     ;;
+  s6)
+    # the LDS-staged device ordered sum: its test, the probe, the driver's line
+    tests_ok timeout -k 10 600 $PYT tests/test_gpu_shard.py > $O/pytest_s6.log 2>&1
+    timeout -k 10 120 python tools/probes/ordered_sum_probe.py > $O/ordered_sum_probe.jsonl &&
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench_s6_k20.json 2> $O/bench_s6_k20.err
+    ;;
+  final)
+    # the final tree: the whole suite and smoke, then the published line with
+    # its same-box profiles -- three PMC passes of the kernel leg (bench
+    # --kernel-only), the line reading them (default K/W and the driver's
+    # K=20 W=5), a kernel trace + stats of the kernel leg restricted to the
+    # timed launches, the f32 PMC passes
+    B="python bench.py --kernel-only --no-cpu --steps 5 --warmup 1"
+    SQC="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_final.log 2>&1
+    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_final.txt 2>&1 &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc64/fetch -o run -- $B > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc64/write -o run -- $B > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc64/sq -o run -- $B > /dev/null &&
+    python tools/pmc_summarize.py $O/pmc64 f64 65536 $O/pmc_l96_f64.json 6 &&
+    timeout -k 10 600 python bench.py --pmc-file $O/pmc_l96_f64.json > $O/bench_line.json 2> $O/bench_line.err &&
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 --pmc-file $O/pmc_l96_f64.json > $O/bench_line_k20.json \
+        2> $O/bench_line_k20.err &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+        python bench.py --kernel-only --no-cpu > $O/bench_kernel_only.json 2> $O/bench_kernel_only.err &&
+    python tools/trace_summary.py $O/trace 200 10 $O/bench_line.json > $O/bench_kernel_trace_summary.json &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc32/fetch -o run -- $B --dtype f32 > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc32/write -o run -- $B --dtype f32 > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc32/sq -o run -- $B --dtype f32 > /dev/null &&
+    python tools/pmc_summarize.py $O/pmc32 f32 65536 $O/pmc_l96_f32.json 6
+    ;;
+  rows)
+    # the configs' and the small ensembles' rows and the reference studies on the final tree
+    timeout -k 10 600 python tools/config_bench.py cfg2@16384 cfg4 cfg4full cfg5 ts6 ts36 > $O/configs_final.jsonl &&
+    timeout -k 10 300 python tools/config_bench.py l96mx1@256 l96mx64@256 l96mx1024@256 l96x1@256 l96x64@256 \
+        > $O/spec_final.jsonl &&
+    for args in "burgers_beta.py 1024" "burgers_beta.py 1" "lorenz_thesis.py 1024" "lorenz_thesis.py 1" \
+                "lorenz63_config2.py" "stuart_reference.py"; do
+      set -- $args
+      timeout -k 10 300 python examples/$1 ${2:-} > $O/ex_tmp.jsonl || exit 1
+      python -c "import json,sys;[print(json.dumps(dict(json.loads(l),example='$1',arg='${2:-}'))) for l in open('$O/ex_tmp.jsonl') if l.startswith('{')]" >> $O/examples_final.jsonl || exit 1
+    done
+    ;;
   *)
     echo "unknown session $1"; exit 2
     ;;
