@@ -264,15 +264,17 @@ __global__ void burn_in_search_kernel(int64_t n_chains, int64_t len, int w, cons
 // strictly in row order, the additions of ipmc_host_ordered_sum (same IEEE
 // operations, -ffp-contract=off: the same bits).  The sum of a column is one
 // dependent chain of adds, so the kernel keeps that chain fed: a block owns 64
-// columns; wave 0 holds one column per lane and adds chunk c (8 192 values)
-// from LDS while waves 1-3 stream chunk c + 1 from global memory into the other
+// columns; wave 0 holds one column per lane and adds chunk c (<= 8 192 values)
+// from LDS while waves 1-15 stream chunk c + 1 from global memory into the other
 // LDS buffer (coalesced, many loads in flight) -- one barrier per chunk.  A
 // lane walking the rows straight from global memory waits out a load latency
 // per row or per unrolled group (2.5 ms for 65 536 x 40 values on the MI355X,
 // more than the host library's one pass).
 constexpr int kOsCols = 64;     // columns per block (wave 0: one per lane)
 constexpr int kOsBuf = 8192;    // doubles per LDS buffer: 8192 / kc rows per chunk
-constexpr int kOsBlock = 256;   // wave 0 adds, waves 1-3 load
+constexpr int kOsBlock = 1024;  // wave 0 adds, waves 1-15 load
+constexpr int kOsLoaders = kOsBlock / 64 - 1;
+constexpr int kOsPerLane = 16;  // rows per loader lane and chunk (>= ceil(8192 / kOsLoaders / 1))
 
 __global__ __launch_bounds__(kOsBlock) void ordered_sum_kernel(const double* __restrict__ x, int64_t n_rows, int64_t k,
                                                               int64_t stride, double div, double* __restrict__ acc) {
@@ -280,18 +282,33 @@ __global__ __launch_bounds__(kOsBlock) void ordered_sum_kernel(const double* __r
   const int t = threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.x * kOsCols;
   const int kc = (int)((k - c0) < kOsCols ? (k - c0) : kOsCols);
-  const int R = kOsBuf / kc;  // rows per chunk
+  // rows per chunk: the buffer's rows, and at most what the loaders cover in one pass
+  const int R = (kOsBuf / kc) < kOsLoaders * kOsPerLane ? (kOsBuf / kc) : kOsLoaders * kOsPerLane;
   const int64_t n_chunks = (n_rows + R - 1) / R;
   auto rows_of = [&](int64_t chunk) {
     const int64_t left = n_rows - chunk * R;
     return (int)(left < R ? left : R);
   };
-  auto load = [&](int64_t chunk, int b) {  // waves 1-3: chunk -> buf[b], row-major [rows][kc]
-    const int64_t r0 = chunk * R;
-    const int n = rows_of(chunk) * kc;
-    for (int i = t - 64; i < n; i += kOsBlock - 64) {
-      const int r = i / kc, j = i - r * kc;
-      buf[b][i] = x[(r0 + r) * stride + c0 + j];
+  // loader lane l of waves 1-15: column l % 64, rows l / 64, + 15, + 30, ...
+  // of the chunk -- all of its loads issued before any LDS write, so each lane
+  // has up to kOsPerLane in flight and the block ~15 x 64 x 16 (no division
+  // per element)
+  const int lj = (t - 64) & 63, lr = (t - 64) >> 6;
+  auto load = [&](int64_t chunk, int b) {  // chunk -> buf[b], row-major [rows][kc]
+    if (lj >= kc) return;
+    const int rows = rows_of(chunk);
+    const double* src = x + chunk * R * stride + c0 + lj;
+    double* dst = buf[b] + lj;
+    double v[kOsPerLane];
+#pragma unroll
+    for (int u = 0; u < kOsPerLane; ++u) {
+      const int r = lr + kOsLoaders * u;
+      v[u] = r < rows ? src[r * stride] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kOsPerLane; ++u) {
+      const int r = lr + kOsLoaders * u;
+      if (r < rows) dst[r * kc] = v[u];
     }
   };
   double a = 0.0;
