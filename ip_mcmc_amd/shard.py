@@ -66,7 +66,7 @@ def _seq_sum(a, acc, div=1.0):
     return acc.reshape(a.shape[1:])
 
 
-def ordered_sum_sharded(local, group=None, div=1.0):
+def ordered_sum_sharded(local, group=None, div=1.0, colsum=None):
     """The sequential sum ((0 + row_0) + row_1) + ... over chains in global
     order when the rows are spread over the ranks in rank order: rank r
     continues rank r-1's running sum (one small message per rank boundary,
@@ -75,9 +75,10 @@ def ordered_sum_sharded(local, group=None, div=1.0):
     gathering them (config 5's per-chain sums are 4 GB).  `local` on the
     device (a CUDA tensor, e.g. MCMCSampler's sums) keeps every hop on the
     device: the sum is ipmc_ordered_sum (the same bits), and only the k totals
-    move -- no host round trip per rank."""
+    move -- no host round trip per rank.  colsum: rank 0's own sum of
+    `local` from zero, already computed (MCMCSampler's last_device_colsum)."""
     if isinstance(local, torch.Tensor) and local.is_cuda:
-        return _ordered_sum_sharded_device(local, group, div)
+        return _ordered_sum_sharded_device(local, group, div, colsum)
     rank, world = world_info(group)
     a = np.asarray(local, dtype=np.float64)
     acc = np.zeros(a.shape[1:], dtype=np.float64)
@@ -97,22 +98,24 @@ def ordered_sum_sharded(local, group=None, div=1.0):
     return t.cpu().numpy()
 
 
-def _ordered_sum_sharded_device(rows, group, div):
+def _ordered_sum_sharded_device(rows, group, div, colsum=None):
     from . import device as D
 
     rank, world = world_info(group)
     rows = rows.reshape(rows.shape[0], -1)
-    acc = torch.zeros(rows.shape[1], dtype=torch.float64, device=rows.device)
+    if rank == 0 and colsum is not None and div == 1.0:
+        acc = colsum  # the same additions from zero, done while the run's results were copied out
+    else:
+        acc = torch.zeros(rows.shape[1], dtype=torch.float64, device=rows.device)
+        if world > 1 and rank > 0:
+            t = torch.empty_like(acc, device=_comm_device(group))
+            dist.recv(t, src=(rank - 1) if group is None else dist.get_global_rank(group, rank - 1), group=group)
+            acc.copy_(t)
+        if rows.shape[0]:
+            D.ordered_sum(rows, acc, div)
     if world > 1:
         comm = _comm_device(group)
         glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
-        if rank > 0:
-            t = torch.empty_like(acc, device=comm)
-            dist.recv(t, src=glob(rank - 1), group=group)
-            acc.copy_(t)
-    if rows.shape[0]:
-        D.ordered_sum(rows, acc, div)
-    if world > 1:
         if rank < world - 1:
             dist.send(acc.to(comm), dst=glob(rank + 1), group=group)
         t = acc.to(comm)
@@ -187,8 +190,10 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     if sampler.chain_offset != lo:
         raise ValueError(f"make_sampler must build the sampler with chain_offset={lo}, got {sampler.chain_offset}")
     # gather="mean": the posterior mean's ordered sum runs on the device sums
-    # the sweeps left (MCMCSampler.last_device_sums) when the run was a device run
-    sampler.keep_device_sums = gather == "mean"
+    # the sweeps left (MCMCSampler.last_device_sums) when the run was a device
+    # run; rank 0 starts the sum from zero, so its run computes it while the
+    # results are copied out (last_device_colsum)
+    sampler.keep_device_sums = ("colsum" if rank == 0 else True) if gather == "mean" else False
     local_u0 = np.asarray(u_0[lo:hi], dtype=np.float64)
     sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
     t0 = time.perf_counter()
@@ -212,8 +217,9 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         n = max(1, res["n"])
         dsum = getattr(sampler, "last_device_sums", None)
         rows = dsum[0] if dsum is not None else res["sum_u"].reshape(hi - lo, k)
-        mean = ordered_sum_sharded(rows, group) / (float(n) * n_total)
-        sampler.last_device_sums = None
+        mean = ordered_sum_sharded(rows, group, colsum=getattr(sampler, "last_device_colsum", None)) / (
+            float(n) * n_total)
+        sampler.last_device_sums = sampler.last_device_colsum = None
         return {"u": cols[0], "phi": phi_all, "accepts": acc_all, "sum_u": res["sum_u"],
                 "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
                 "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,

@@ -112,7 +112,8 @@ def _mean_worker(rank, world, port, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="mean")
-    assert res["sampler"].last_path == "device" and res["sampler"].last_device_sums is None
+    s = res["sampler"]
+    assert s.last_path == "device" and s.last_device_sums is None and s.last_device_colsum is None
     if rank == 1:
         np.savez(out_path, mean=res["mean"], phi=res["phi"], acc=res["accepts"])
     dist.barrier()
@@ -132,7 +133,8 @@ def _make_sampler(chain_offset=0):
 
 def test_run_sharded_mean_on_the_device_equals_the_host_mean(tmp_path):
     """gather='mean' sums the sweeps' device sums (ipmc_ordered_sum, rank by
-    rank): one process and two ranks (gloo hops, both on cuda:0) give the host
+    rank; rank 0's sum computed by its run while the results are copied out):
+    one process and two ranks (gloo hops, both on cuda:0) give the host
     ordered mean of the per-chain sums bit for bit."""
     from ip_mcmc_amd.shard import _seq_sum, run_sharded
 
