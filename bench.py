@@ -327,17 +327,23 @@ def sampler_factory(prob, dtype_np, dev, seed=2):
     return make
 
 
-def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="all", seed=2):
+def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="all", seed=2, settle=None):
     """SURVEY §8(d)'s timed region: shard.run_sharded(u_0 on the host, exactly
     `steps` pCN steps, keep='moments') bracketed by barrier + synchronize,
-    after an untimed run of `warmup` steps of the same shape.  Returns the
-    record and the gathered result."""
+    after an untimed run of `warmup` steps of the same shape and `settle()`
+    (the kernel leg's untimed G evaluations: the clocks drop within the ~10 ms
+    the host takes between legs and ramp back over ~0.1-0.3 s, so the timed
+    run of a K=20 line otherwise starts on them: 3.35 instead of 3.2 ms per
+    step, profiles/r5/e2e_trace_summary.json).  Returns the record and the
+    gathered result."""
     from ip_mcmc_amd.shard import run_sharded
 
     make = sampler_factory(prob, dtype_np, dev, seed)
     u0 = np.full((total_chains, prob.k), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch)
     if warmup > 0:
         run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=warmup, keep="moments", gather=gather)
+    if settle is not None:
+        settle()
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
@@ -555,7 +561,9 @@ def main():
     kernel_rate = total_chains * steps / el_k
     log(f"kernel leg: {el_k:.3f} s, kernel {kern_ms:.3f} ms/launch, {kernel_rate / 1e6:.2f} M steps/s")
     lanes_k, cpl_k, spec_k = w.lanes, w.chains_per_lane, w.spec_width
-    del w
+    # the end-to-end legs settle the clocks on the kernel leg's chains (their
+    # swept state, untouched: ipmc_potential into a scratch Φ)
+    settle = lambda: w.settle_clocks(args.settle)  # noqa: E731
     if args.kernel_only:
         args.no_extra = args.no_configs = args.no_cpu = True
 
@@ -570,7 +578,7 @@ def main():
         res = {"phi": np.zeros(0), "mean": np.zeros(0), "accepts": np.zeros(0)}
     else:
         log(f"end-to-end leg: run_sharded({total_chains} chains, {steps} steps, keep='moments', gather={gather_mode})")
-        e2e, res = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode)
+        e2e, res = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode, settle=settle)
     value = e2e["pcn_steps_per_s"]
     log(f"end-to-end: {e2e['wall_s']:.3f} s, {value / 1e6:.2f} M steps/s")
     gather = {"ms": e2e["gather_ms"], "mode": gather_mode,
@@ -620,7 +628,7 @@ def main():
         extra[f"{key}_kernel_tflops"] = per_rank * per_launch * prob.flop / (k2 * 1e-3) / 1e12
         del w2
         e2 = timed_run(prob, np.float32 if key == "f32" else np.float64, dev, total_chains, min(steps, 100), 2,
-                       world, gather=gather_mode)[0]
+                       world, gather=gather_mode, settle=settle)[0]
         extra[f"{key}_run_pcn_steps_per_s"] = e2["pcn_steps_per_s"]
         # the reference's operation order (no FMA in the forward map): the
         # arithmetic whose accept streams are pinned to the reference fixtures
@@ -634,20 +642,21 @@ def main():
         extra["reference_arith_kernel_tflops"] = per_rank * per_launch * prob.flop / (k3 * 1e-3) / 1e12
         del w3
         # REFERENCE arith end to end: the same timed region as value
-        er = timed_run(pref, ndt, dev, total_chains, steps, 2, world, gather=gather_mode)[0]
+        er = timed_run(pref, ndt, dev, total_chains, steps, 2, world, gather=gather_mode, settle=settle)[0]
         log(f"reference arith end to end: {er['pcn_steps_per_s'] / 1e6:.2f} M steps/s")
         parity["reference_arith_value"] = er["pcn_steps_per_s"]
         parity["reference_arith_run_e2e_moments"] = er
         # the headline's shape and kernel on a posterior the chains sample
         # (the rate should not depend on acceptance)
         pmix = make_problem("cfg3_mixing")
-        em = timed_run(pmix, ndt, dev, total_chains, steps, 2, world, gather=gather_mode)[0]
+        em = timed_run(pmix, ndt, dev, total_chains, steps, 2, world, gather=gather_mode, settle=settle)[0]
         log(f"mixing posterior end to end: {em['pcn_steps_per_s'] / 1e6:.2f} M steps/s, "
             f"{em['accept_rate']:.3f} accepted")
         extra["mixing_posterior"] = dict(em, workload=pmix.name, data=pmix.data, over_value=em["pcn_steps_per_s"] / value,
                                          accept_rate_value=accept_rate)
         if world > 1:  # weak scaling beside the strong line: 65 536 chains per GPU
-            wk, _ = timed_run(prob, ndt, dev, world * CHAINS_PER_GPU, min(steps, 40), 2, world, gather=gather_mode)
+            wk, _ = timed_run(prob, ndt, dev, world * CHAINS_PER_GPU, min(steps, 40), 2, world, gather=gather_mode,
+                              settle=settle)
             extra["weak_scaling"] = {"pcn_steps_per_s": wk["pcn_steps_per_s"], "total_chains": world * CHAINS_PER_GPU,
                                      "ms_per_step": wk["ms_per_step"], "steps": wk["steps"],
                                      "timed": "run_sharded end to end, keep='moments'"}
@@ -658,6 +667,7 @@ def main():
             log(f"extra.configs: {key} end to end")
             cfgs[key] = config_line(key, dev, world)
         extra["configs"] = cfgs
+    del settle, w
 
     flop = per_rank * per_launch * prob.flop
     achieved = flop / (kern_ms * 1e-3) / 1e12
@@ -717,6 +727,8 @@ def main():
                     "reference_arith_value": parity.get("reference_arith_value")},
                 "parallelism": f"{total_chains} chains sharded over {world} GPU(s) ({args.scaling} scaling)",
                 "clock_settle_s": args.settle,
+                "clock_settle": "untimed G evaluations of the kernel leg's chains before the kernel leg's and before "
+                                "each end-to-end leg's timed region (after its warm-up run)",
             },
             "roofline": {
                 "bound": "valu",

@@ -126,6 +126,22 @@ case "$1" in
     timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/pmc32/sq -o run -- $B --dtype f32 > /dev/null &&
     python tools/pmc_summarize.py $O/pmc32 f32 65536 $O/pmc_l96_f32.json 6
     ;;
+  e2etrace)
+    # kernel + copy trace of the driver's K=20 line (end-to-end leg included):
+    # per-launch sweep times inside run() against the kernel leg's, the gaps
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/e2etrace -o run -- \
+      python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity > $O/e2etrace.json \
+      2> $O/e2etrace.err
+    ;;
+  settle)
+    # end-to-end legs with the clocks settled before their timed region: the
+    # driver's K=20 line, then the kernel + copy trace of a short line
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 --pmc-file profiles/r5/pmc_l96_f64.json \
+      > $O/bench_settle_k20.json 2> $O/bench_settle_k20.err &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/e2etrace_settle -o run -- \
+      python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity > $O/e2etrace_settle.json \
+      2> $O/e2etrace_settle.err
+    ;;
   rows)
     # the configs' and the small ensembles' rows and the reference studies on the final tree
     timeout -k 10 600 python tools/config_bench.py cfg2@16384 cfg4 cfg4full cfg5 ts6 ts36 > $O/configs_final.jsonl &&
