@@ -12,10 +12,13 @@ reject.  value is SURVEY §8(d)'s timed region: the drop-in
 every chain in the fused libipmc kernels, the posterior-mean sums and the
 chain state back to the host (D2H), and the final gather over the ranks
 (RCCL at N > 1) -- bracketed by barrier + synchronize, max over ranks.
-value = all chains of all ranks x K / that time.  The metric's 65 536 chains
-are split over the N GPUs (strong scaling, the default; global chain ids, so
-every chain is the one-GPU run's bit for bit); the weak number (65 536 chains
-per GPU) is carried in "extra" for N > 1.
+value = all chains of all ranks x K / that time.  The chains are independent
+units, sharded over the ranks with no collective on the data path (global
+chain ids, so every chain is the one-GPU run's bit for bit): cfg3 runs the
+metric's 65 536 chains on every GPU (weak scaling, the default), and at N > 1
+"extra.strong_scaling" carries the 65 536 chains split over the N GPUs.
+Configs 4 and 5 state their ensembles per node, so --workload cfg4 / cfg5
+split them (strong).
 
 extra.kernel_*: the same sweep kernel on device-resident state (raw
 ipmc_pcn_sweep launches, one pCN step per launch for a full GPU, HIP events
@@ -490,9 +493,9 @@ def main():
                          "chains; cfg5: Lorenz-96 d=256, 10 000 RK4 steps, 2^20 chains (f32 beside f64)")
     ap.add_argument("--chains", type=int, default=None,
                     help="total chains (strong, the default) or chains per GPU (weak); default: the workload's")
-    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
-                    help="strong: --chains split over the GPUs (the metric's 65 536; default); "
-                         "weak: --chains per GPU")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="weak: --chains per GPU (cfg3's default: 65 536 chains on every GPU); strong: --chains "
+                         "split over the GPUs (cfg4 / cfg5's default: their ensembles are stated per node)")
     ap.add_argument("--steps-per-launch", type=int, default=0,
                     help="pCN steps per kernel launch of the kernel leg (0 = auto)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
@@ -543,6 +546,8 @@ def main():
     steps = args.steps if args.steps is not None else prob.steps
     warmup = args.warmup if args.warmup is not None else prob.warmup
     chains = args.chains or prob.chains
+    if args.scaling is None:
+        args.scaling = "weak" if args.workload == "cfg3" else "strong"
     total_chains = chains * (world if args.scaling == "weak" else 1)
     if total_chains % world:
         raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
@@ -654,12 +659,13 @@ def main():
             f"{em['accept_rate']:.3f} accepted")
         extra["mixing_posterior"] = dict(em, workload=pmix.name, data=pmix.data, over_value=em["pcn_steps_per_s"] / value,
                                          accept_rate_value=accept_rate)
-        if world > 1:  # weak scaling beside the strong line: 65 536 chains per GPU
-            wk, _ = timed_run(prob, ndt, dev, world * CHAINS_PER_GPU, min(steps, 40), 2, world, gather=gather_mode,
-                              settle=settle)
-            extra["weak_scaling"] = {"pcn_steps_per_s": wk["pcn_steps_per_s"], "total_chains": world * CHAINS_PER_GPU,
-                                     "ms_per_step": wk["ms_per_step"], "steps": wk["steps"],
-                                     "timed": "run_sharded end to end, keep='moments'"}
+        if world > 1:  # the other scaling beside the line: 65 536 chains per GPU / over the node
+            other_s = "strong" if args.scaling == "weak" else "weak"
+            n_other = CHAINS_PER_GPU * (world if other_s == "weak" else 1)
+            wk, _ = timed_run(prob, ndt, dev, n_other, steps, 2, world, gather=gather_mode, settle=settle)
+            extra[f"{other_s}_scaling"] = {"pcn_steps_per_s": wk["pcn_steps_per_s"], "total_chains": n_other,
+                                           "chains_per_gpu": n_other // world, "ms_per_step": wk["ms_per_step"],
+                                           "steps": wk["steps"], "timed": "run_sharded end to end, keep='moments'"}
         extra["run_e2e_samples"] = e2e_samples(prob, per_rank, rank * per_rank, ndt, dev, world)
     if not args.no_configs and args.workload == "cfg3":
         cfgs = {}

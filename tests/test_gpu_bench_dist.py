@@ -3,7 +3,8 @@ the final gather, rank-0 JSON line) rehearsed with 2 ranks on the one-GPU box:
 both ranks on cuda:0 and gloo for the collectives (RCCL needs one GPU per rank;
 the driver's 8-GPU runs use it).  Started both ways: under an external
 torch.distributed.run (the driver's form) and as plain `python bench.py --gpus 2`,
-which launches the ranks itself (strong scaling on the metric's 65 536 chains),
+which launches the ranks itself (weak scaling: the metric's 65 536 chains on every
+rank, the strong split beside it),
 and the config-5 workload (2^20 chains over the ranks, f64, through
 shard.run_sharded with the rank-sequential posterior mean)."""
 import json
@@ -52,16 +53,17 @@ def test_bench_gpus_2_launches_its_own_ranks():
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
-    assert line["config"]["total_chains"] == 65536 and line["config"]["chains_per_gpu"] == 32768
-    assert line["final_gather"]["rows"] == 65536 and line["final_gather"]["inside_timed_region"]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["total_chains"] == 131072 and line["config"]["chains_per_gpu"] == 65536
+    assert line["final_gather"]["rows"] == 131072 and line["final_gather"]["inside_timed_region"]
     ex = line["extra"]
-    assert ex["weak_scaling"]["total_chains"] == 131072 and ex["weak_scaling"]["pcn_steps_per_s"] > 0
+    assert ex["strong_scaling"]["total_chains"] == 65536 and ex["strong_scaling"]["chains_per_gpu"] == 32768
+    assert ex["strong_scaling"]["pcn_steps_per_s"] > 0
     assert ex["reference_arith_kernel_pcn_steps_per_s"] > 0 and ex["run_e2e_samples"]["pcn_steps_per_s"] > 0
     # value is the end-to-end run; the kernel leg is beside it
     assert line["value"] == ex["run_e2e_moments"]["pcn_steps_per_s"] and ex["kernel_pcn_steps_per_s"] > 0
     assert abs(line["ms_per_step"] * line["steps"] / 1e3 - ex["run_e2e_moments"]["wall_s"]) < 1e-9
-    assert ex["mixing_posterior"]["total_chains"] == 65536 and ex["mixing_posterior"]["pcn_steps_per_s"] > 0
+    assert ex["mixing_posterior"]["total_chains"] == 131072 and ex["mixing_posterior"]["pcn_steps_per_s"] > 0
     # REFERENCE arith end to end beside value; the paired streams run at N = 1 only
     assert line["parity"]["reference_arith_value"] > 0 and "paired_identical_accept_frac" not in line["parity"]
     assert ex["configs"]["cfg4"]["f64"]["total_chains"] == 16384

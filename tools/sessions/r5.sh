@@ -134,8 +134,10 @@ case "$1" in
       2> $O/e2etrace.err
     ;;
   settle)
-    # end-to-end legs with the clocks settled before their timed region: the
-    # driver's K=20 line, then the kernel + copy trace of a short line
+    # end-to-end legs with the clocks settled before their timed region, weak
+    # scaling by default: the N-rank and shard tests, the driver's K=20 line,
+    # then the kernel + copy trace of a short line
+    tests_ok timeout -k 10 900 $PYT tests/test_gpu_bench_dist.py tests/test_gpu_shard.py > $O/pytest_settle.log 2>&1
     timeout -k 10 600 python bench.py --steps 20 --warmup 5 --pmc-file profiles/r5/pmc_l96_f64.json \
       > $O/bench_settle_k20.json 2> $O/bench_settle_k20.err &&
     timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/e2etrace_settle -o run -- \
