@@ -144,6 +144,16 @@ case "$1" in
       python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity > $O/e2etrace_settle.json \
       2> $O/e2etrace_settle.err
     ;;
+  f32ab)
+    # the packed fp32 headline sweep: the round-5-start build of its unit
+    # (variants/r5start, identical ISA by hipcc -S) against the product,
+    # interleaved three times -- is the 1.70 -> 1.95 ms move the box or the code?
+    for i in 1 2 3; do
+      timeout -k 10 120 python tools/probes/arith_kernel_probe.py product 40 f32 >> $O/f32_ab.jsonl &&
+      IPMC_LIB_PATH=ip_mcmc_amd/lib/variants/r5start/libipmc.so timeout -k 10 120 \
+          python tools/probes/arith_kernel_probe.py r5start 40 f32 >> $O/f32_ab.jsonl || exit 1
+    done
+    ;;
   rows)
     # the configs' and the small ensembles' rows and the reference studies on the final tree
     timeout -k 10 600 python tools/config_bench.py cfg2@16384 cfg4 cfg4full cfg5 ts6 ts36 > $O/configs_final.jsonl &&
