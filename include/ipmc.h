@@ -30,8 +30,8 @@
  *                                     lorenz_mcmc.py:17-40
  *   MCMCSampler.autocorr              sampler.py:43-54        ipmc_autocorr
  *   len_burn_in                       burgers/utilities.py:134-167  ipmc_burn_in
- *   np.mean over the samples          sampler.py:20-28 callers ipmc_ordered_sum (the many-chain posterior
- *                                     (e.g. stuart_examples.py)  mean's chain-ordered sum, on the device)
+ *   np.mean over the samples          sampler.py:20-28 callers ipmc_block_sums (the many-chain posterior
+ *                                     (e.g. stuart_examples.py)  mean's fixed-order block sums, on the device)
  *
  * The reference has no FFI of its own (it is duck-typed Python); these entry
  * points are what a ctypes binding of its plugin API binds.
@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define IPMC_ABI_VERSION 12
+#define IPMC_ABI_VERSION 13
 
 typedef enum {
   IPMC_OK = 0,
@@ -255,6 +255,14 @@ int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars,
    div == 1 adds the rows as they are.  Device pointers; acc [k] in/out. */
 int ipmc_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div, double* acc,
                      void* stream);
+
+/* (ABI 13) out[b][j] = (((0 + rows[bB][j]/div) + rows[bB+1][j]/div) + ...) for j < k over the rows of block b
+   (B = block_rows consecutive rows; the last block holds the n_rows % B left over), each block from zero
+   strictly in row order -- the first stage of the many-chain posterior mean (shard.block_sum: block sums,
+   then the block sums in block order), equal bit for bit to ipmc_host_ordered_sum on each block from zero.
+   Blocks run in parallel.  Device pointers; out [ceil(n_rows / B), k]. */
+int ipmc_block_sums(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, int64_t block_rows,
+                    double div, double* out, void* stream);
 
 /* Lorenz-96 layout of a ONE-step launch (no speculation) when lanes_per_chain = chains_per_lane = 0:
    returns lanes_per_chain, and chains_per_lane * 100 + lanes_per_chain from ipmc_auto_layout.

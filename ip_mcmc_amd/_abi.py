@@ -4,7 +4,7 @@ Only layout and constants live here; compute goes through ``_lib``.
 """
 import ctypes as C
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_DEVICE = 0, 1, 2, 3
 F32, F64 = 0, 1
@@ -132,6 +132,8 @@ SIGNATURES = {
     ),
     "ipmc_ordered_sum": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_void_p,
                                    C.c_void_p]),
+    "ipmc_block_sums": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_void_p,
+                                  C.c_void_p]),
     "ipmc_auto_lanes": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_auto_layout": (C.c_int, [C.POINTER(IpmcModel), C.c_int32, C.c_int64]),
     "ipmc_plan_sweep": (C.c_int, [C.POINTER(IpmcModel), C.POINTER(IpmcSweep), C.POINTER(IpmcPlan)]),

@@ -92,6 +92,27 @@ def ordered_sum(rows, acc, div=1.0):
     return acc
 
 
+def block_sums(rows, block, div=1.0):
+    """out[b] = rows[bB]/div + rows[bB+1]/div + ... from zero in row order over
+    each block of B = `block` consecutive rows (the last one possibly shorter),
+    on the device (ipmc_block_sums, the current stream): the bits of the host
+    library's ipmc_host_ordered_sum on each block.  rows: device f64 [n, k] with
+    unit column stride; returns a new device f64 [ceil(n / B), k]."""
+    if rows.dtype != torch.float64 or rows.dim() != 2:
+        raise ValueError("block_sums needs f64 rows [n, k]")
+    if block <= 0:
+        raise ValueError("block_sums: block must be positive")
+    n, k = rows.shape
+    out = torch.empty(((n + block - 1) // block, k), dtype=torch.float64, device=rows.device)
+    if n == 0 or k == 0:
+        return out
+    if rows.stride(1) != 1:
+        raise ValueError("block_sums needs rows with contiguous columns")
+    call("ipmc_block_sums", rows.data_ptr(), n, k, rows.stride(0), int(block), float(div), out.data_ptr(),
+         stream_handle(rows.device))
+    return out
+
+
 def normals(seed, chain_offset, n_chains, step, k, dtype=None, device=None):
     device = resolve_device(device)
     td = torch_dtype(dtype)

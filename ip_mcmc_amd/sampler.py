@@ -151,11 +151,9 @@ class MCMCSampler:
         self.last_run_seconds = None
         # keep_device_sums: a keep="moments" device run leaves its (sum_u,
         # sum_u2) device tensors in last_device_sums (shard.run_sharded sums
-        # them on the device for the posterior mean); "colsum" also leaves
-        # their chain-ordered column sum from zero in last_device_colsum
-        # (computed while the results are copied out); off by default
+        # them on the device for the posterior mean); off by default
         self.keep_device_sums = False
-        self.last_device_sums = self.last_device_colsum = None
+        self.last_device_sums = None
         # "device" (fused kernels), "host" / "host-generic" (hostloop.py) for the last run
         self.last_path = None
         self.last_run_timing = None
@@ -176,7 +174,7 @@ class MCMCSampler:
         if keep not in ("samples", "moments", "last"):
             raise ValueError("keep must be 'samples', 'moments' or 'last'")
         t_entry = time.perf_counter()
-        self.last_device_sums = self.last_device_colsum = None
+        self.last_device_sums = None
         try:
             plan = _Plan(self.proposer, self.accepter)
         except UnsupportedOnDevice as e:
@@ -421,16 +419,6 @@ class MCMCSampler:
             writer.finish()
         ev_swept = torch.cuda.Event(enable_timing=True)
         ev_swept.record(torch.cuda.current_stream(device))
-        # keep_device_sums == "colsum": the chain-ordered column sum of sum_u
-        # from zero (the posterior mean's numerator on rank 0 / one rank), on a
-        # side stream while the state and sums are copied to the host
-        colsum = None
-        if keep == "moments" and self.keep_device_sums == "colsum":
-            side = torch.cuda.Stream(device=device)
-            side.wait_event(ev_swept)
-            with torch.cuda.stream(side):
-                colsum = torch.zeros(k, dtype=torch.float64, device=device)
-                dev.ordered_sum(sums[0], colsum)
         # the host copy of the samples goes to page-locked memory (~57 GB/s
         # instead of ~5 GB/s pageable on the MI355X box, profiles/r1/d2h_probe.txt);
         # allocating it here overlaps the allocation with the queued sweeps
@@ -496,7 +484,6 @@ class MCMCSampler:
             out = host_out.numpy()  # shares the page-locked buffer (kept alive by the array)
             return out[0] if single else out
         self.last_device_sums = sums if (keep == "moments" and self.keep_device_sums) else None
-        self.last_device_colsum = colsum
         if keep == "moments":
             n_post = n_samples * sample_interval
             res = {"sum_u": sums_host[0].numpy(), "sum_u2": sums_host[1].numpy(), "n": n_post}

@@ -7,8 +7,9 @@ so every chain's trajectory is bitwise identical for any P.  The only
 collective is the final gather of per-chain results to every rank
 (``torch.distributed.all_gather_into_tensor``; backend "nccl" = RCCL over
 xGMI on MI355X, "gloo" on CPU) and a reduction in fixed global chain order
-(rank-sequential, on the device when the sums are; ipmc_ordered_sum /
-ipmc_host_ordered_sum, the same bits), so posterior means are also bitwise
+(fixed blocks of chains summed in parallel -- on the device when the sums
+are, ipmc_block_sums -- then the block sums in order; ipmc_host_ordered_sum
+gives the host the same bits), so posterior means are also bitwise
 independent of P.
 """
 import os
@@ -45,14 +46,41 @@ def gather_chains(local, n_total, group=None):
     return torch.cat(parts, dim=0)
 
 
-def ordered_mean(x, div=1.0):
-    """Mean over the chain axis (dim 0) in fixed sequential chain order, on the
-    host in float64: identical for every sharding of the same chains.  The
-    running sum ((0 + row_0/div) + row_1/div) + ... is ipmc_host_ordered_sum
-    (libipmc_host.so: one pass, ~1 ms for 65 536 x 40; a blocked np.cumsum of
-    the same additions took 40 ms, inside bench.py's timed region)."""
+# Chains per block of the posterior-mean sum.  Fixed, so the order of the
+# additions -- and the bits of the mean -- does not depend on how the chains
+# are sharded; the blocks are summed in parallel.
+MEAN_BLOCK = 1024
+
+
+def ordered_mean(x, div=1.0, block=MEAN_BLOCK):
+    """Mean over the chain axis (dim 0) in a fixed order (block_sum), on the
+    host in float64: identical for every sharding of the same chains."""
     a = x.detach().double().cpu().numpy() if hasattr(x, "detach") else np.asarray(x, dtype=np.float64)
-    return _seq_sum(a, np.zeros(a.shape[1:], dtype=np.float64), div) / a.shape[0]
+    return block_sum(a, div, block) / a.shape[0]
+
+
+def block_sum(a, div=1.0, block=MEAN_BLOCK):
+    """The posterior mean's sum over the chain axis in its fixed order: the rows
+    of each block of `block` consecutive chains added from zero in row order
+    (S_b = ((0 + x_bB/div) + x_bB+1/div) + ...), then the block sums in block
+    order ((0 + S_0) + S_1) + ... .  One block (<= `block` chains) is the plain
+    sequential sum.  ordered_sum_sharded forms the same additions over the
+    ranks' rows (device: ipmc_block_sums), so the bits do not depend on the
+    number of ranks."""
+    a = np.asarray(a, dtype=np.float64)
+    k = int(np.prod(a.shape[1:], dtype=np.int64))
+    rows = a.reshape(a.shape[0], k)
+    return _seq_sum(_host_block_sums(rows, div, block), np.zeros(k)).reshape(a.shape[1:])
+
+
+def _host_block_sums(rows, div, block):
+    """[ceil(n / block), k]: each block's rows from zero in row order
+    (ipmc_host_ordered_sum; ipmc_block_sums is the device twin)."""
+    nb = -(-rows.shape[0] // block)
+    out = np.empty((nb, rows.shape[1]), dtype=np.float64)
+    for b in range(nb):
+        out[b] = _seq_sum(rows[b * block : (b + 1) * block], np.zeros(rows.shape[1]), div)
+    return out
 
 
 def _seq_sum(a, acc, div=1.0):
@@ -66,62 +94,95 @@ def _seq_sum(a, acc, div=1.0):
     return acc.reshape(a.shape[1:])
 
 
-def ordered_sum_sharded(local, group=None, div=1.0, colsum=None):
-    """The sequential sum ((0 + row_0) + row_1) + ... over chains in global
-    order when the rows are spread over the ranks in rank order: rank r
-    continues rank r-1's running sum (one small message per rank boundary,
-    send/recv), and the last rank's total is broadcast to every rank.
-    Bit-identical to ordered_mean's sum over the gathered rows, without
-    gathering them (config 5's per-chain sums are 4 GB).  `local` on the
-    device (a CUDA tensor, e.g. MCMCSampler's sums) keeps every hop on the
-    device: the sum is ipmc_ordered_sum (the same bits), and only the k totals
-    move -- no host round trip per rank.  colsum: rank 0's own sum of
-    `local` from zero, already computed (MCMCSampler's last_device_colsum)."""
-    if isinstance(local, torch.Tensor) and local.is_cuda:
-        return _ordered_sum_sharded_device(local, group, div, colsum)
+def _segments(lo, hi, block):
+    """[lo, hi) cut at the multiples of `block`: (start, stop, whole block?)."""
+    segs, s = [], lo
+    while s < hi:
+        e = min(hi, (s // block + 1) * block)
+        segs.append((s, e, e - s == block))
+        s = e
+    return segs
+
+
+def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
+    """block_sum over the chains of all ranks in global (rank) order, each rank
+    holding its own rows: a rank sums its whole blocks (on the device when
+    `local` is a CUDA tensor: ipmc_block_sums, one launch) and contributes those
+    sums plus the raw rows of the (at most two) blocks it shares with other
+    ranks to one all_gather; every rank then finishes the same additions on the
+    host (the shared blocks' rows in rank order, then the block sums in block
+    order).  Bit-identical to block_sum over the gathered rows, without
+    gathering them (config 5's per-chain sums are 4 GB), and no rank waits on
+    another's sum: one all_gather of ~k / block of the data instead of P - 1
+    sequential hops."""
     rank, world = world_info(group)
-    a = np.asarray(local, dtype=np.float64)
-    acc = np.zeros(a.shape[1:], dtype=np.float64)
-    if world == 1:
-        return _seq_sum(a, acc, div)
-    dev = _comm_device(group)
-    glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
-    if rank > 0:
-        t = torch.empty(acc.shape, dtype=torch.float64, device=dev)
-        dist.recv(t, src=glob(rank - 1), group=group)
-        acc = t.cpu().numpy()
-    acc = _seq_sum(a, acc, div)
-    if rank < world - 1:
-        dist.send(torch.from_numpy(acc).to(dev), dst=glob(rank + 1), group=group)
-    t = torch.from_numpy(np.ascontiguousarray(acc)).to(dev)
-    dist.broadcast(t, src=glob(world - 1), group=group)
-    return t.cpu().numpy()
-
-
-def _ordered_sum_sharded_device(rows, group, div, colsum=None):
-    from . import device as D
-
-    rank, world = world_info(group)
-    rows = rows.reshape(rows.shape[0], -1)
-    if rank == 0 and colsum is not None and div == 1.0:
-        acc = colsum  # the same additions from zero, done while the run's results were copied out
+    on_dev = isinstance(local, torch.Tensor) and local.is_cuda
+    shape = tuple(local.shape[1:])
+    k = int(np.prod(shape, dtype=np.int64))
+    if on_dev:
+        rows = local.reshape(local.shape[0], k)
     else:
-        acc = torch.zeros(rows.shape[1], dtype=torch.float64, device=rows.device)
-        if world > 1 and rank > 0:
-            t = torch.empty_like(acc, device=_comm_device(group))
-            dist.recv(t, src=(rank - 1) if group is None else dist.get_global_rank(group, rank - 1), group=group)
-            acc.copy_(t)
-        if rows.shape[0]:
-            D.ordered_sum(rows, acc, div)
+        a = local.detach().cpu().numpy() if isinstance(local, torch.Tensor) else local
+        rows = np.asarray(a, dtype=np.float64).reshape(len(a), k)
+    n_local = int(rows.shape[0])
     if world > 1:
-        comm = _comm_device(group)
-        glob = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
-        if rank < world - 1:
-            dist.send(acc.to(comm), dst=glob(rank + 1), group=group)
-        t = acc.to(comm)
-        dist.broadcast(t, src=glob(world - 1), group=group)
-        acc = t
-    return acc.cpu().numpy()
+        dev = _comm_device(group)
+        counts = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(counts, torch.tensor([n_local], dtype=torch.int64, device=dev), group=group)
+        counts = counts.cpu().tolist()
+    else:
+        counts = [n_local]
+    los = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    lo = int(los[rank])
+    segs = _segments(lo, lo + n_local, block)
+    whole = [(s0, e0) for s0, e0, w in segs if w]
+    if whole:  # a rank's whole blocks are consecutive
+        f0, f1 = whole[0][0] - lo, whole[-1][1] - lo
+        if on_dev:
+            from . import device as D
+
+            F = D.block_sums(rows[f0:f1], block, div).cpu().numpy()
+        else:
+            F = _host_block_sums(rows[f0:f1], div, block)
+    else:
+        F = np.zeros((0, k))
+    shared = [rows[s0 - lo : e0 - lo] for s0, e0, w in segs if not w]
+    shared = [p.cpu().numpy() if on_dev else p for p in shared]
+    mine = np.concatenate([F.reshape(-1)] + [p.reshape(-1) for p in shared]) if (len(F) or shared) else np.zeros(0)
+    if world > 1:
+        sizes = []
+        for r in range(world):
+            sr = _segments(int(los[r]), int(los[r + 1]), block)
+            sizes.append(sum(1 if w else (e0 - s0) for s0, e0, w in sr) * k)
+        per = max(max(sizes), 1)
+        buf = torch.zeros(per, dtype=torch.float64, device=dev)
+        buf[: mine.size] = torch.from_numpy(mine).to(dev)
+        allb = torch.empty(per * world, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allb, buf, group=group)
+        allb = allb.cpu().numpy().reshape(world, per)
+        parts = [allb[r] for r in range(world)]
+    else:
+        parts = [mine]
+    n_total = int(los[-1])
+    sums = np.zeros((-(-n_total // block), k), dtype=np.float64)
+    pieces = {}
+    for r in range(world):
+        off = 0
+        sr = _segments(int(los[r]), int(los[r + 1]), block)
+        nw = sum(1 for _, _, w in sr if w)
+        Fr = parts[r][: nw * k].reshape(nw, k)
+        off, i = nw * k, 0
+        for s0, e0, w in sr:
+            if w:
+                sums[s0 // block] = Fr[i]
+                i += 1
+            else:
+                m = (e0 - s0) * k
+                pieces.setdefault(s0 // block, []).append(parts[r][off : off + m].reshape(e0 - s0, k))
+                off += m
+    for b, pc in pieces.items():  # a block over several ranks: its rows in rank order, from zero
+        sums[b] = _seq_sum(np.concatenate(pc), np.zeros(k), div)
+    return _seq_sum(sums, np.zeros(k)).reshape(shape)
 
 
 def world_info(group=None):
@@ -158,7 +219,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
       "u", "phi", "accepts"   the final chain states (C_total, k), Φ, accept counts
       keep="moments": "sum_u", "sum_u2" (C_total, k) and "n", plus "mean"
                      (the posterior-mean estimate: the per-chain sums added
-                     over the chains in fixed global order, ordered_mean, over
+                     over the chains in a fixed order, block_sum, over
                      n x C_total -- bit-identical for any number of ranks)
       keep="samples": "samples" (C_total, n_samples, k); with sample_file each
                      rank streams its own block to f"{sample_file}.rank{r}.npy"
@@ -168,7 +229,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
       "sampler" (this rank's sampler, state included), "run_seconds" (this
       rank's run()), "gather_seconds".
     gather="mean" (keep="moments" only) gathers just Φ and the accept counts
-    and forms "mean" by the rank-sequential ordered_sum_sharded, for ensembles
+    and forms "mean" by ordered_sum_sharded (block sums), for ensembles
     whose per-chain arrays are too large to copy to every rank (config 5:
     2^20 chains x 256); "u", "sum_u", "sum_u2" are then this rank's rows only.
     With one rank (no process group) it is a plain run()."""
@@ -189,11 +250,9 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     sampler = make_sampler(chain_offset=lo)
     if sampler.chain_offset != lo:
         raise ValueError(f"make_sampler must build the sampler with chain_offset={lo}, got {sampler.chain_offset}")
-    # gather="mean": the posterior mean's ordered sum runs on the device sums
-    # the sweeps left (MCMCSampler.last_device_sums) when the run was a device
-    # run; rank 0 starts the sum from zero, so its run computes it while the
-    # results are copied out (last_device_colsum)
-    sampler.keep_device_sums = ("colsum" if rank == 0 else True) if gather == "mean" else False
+    # gather="mean": the posterior mean's block sums run on the device sums the
+    # sweeps left (MCMCSampler.last_device_sums) when the run was a device run
+    sampler.keep_device_sums = gather == "mean"
     local_u0 = np.asarray(u_0[lo:hi], dtype=np.float64)
     sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
     t0 = time.perf_counter()
@@ -217,9 +276,8 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         n = max(1, res["n"])
         dsum = getattr(sampler, "last_device_sums", None)
         rows = dsum[0] if dsum is not None else res["sum_u"].reshape(hi - lo, k)
-        mean = ordered_sum_sharded(rows, group, colsum=getattr(sampler, "last_device_colsum", None)) / (
-            float(n) * n_total)
-        sampler.last_device_sums = sampler.last_device_colsum = None
+        mean = ordered_sum_sharded(rows, group) / (float(n) * n_total)
+        sampler.last_device_sums = None
         return {"u": cols[0], "phi": phi_all, "accepts": acc_all, "sum_u": res["sum_u"],
                 "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
                 "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
@@ -254,8 +312,8 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         elif keep == "last":
             out["last"] = rest
     if keep == "moments":
-        # Σ over chains (in global order) of the per-chain sums, / (steps × chains) once
-        S = _seq_sum(np.asarray(out["sum_u"]), np.zeros(k))
+        # Σ over chains (block_sum's fixed order) of the per-chain sums, / (steps × chains) once
+        S = block_sum(np.asarray(out["sum_u"]))
         out["mean"] = S / (float(max(1, res["n"])) * n_total)
     out["gather_seconds"] = time.perf_counter() - t1
     return out

@@ -113,7 +113,7 @@ def _mean_worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     res = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="mean")
     s = res["sampler"]
-    assert s.last_path == "device" and s.last_device_sums is None and s.last_device_colsum is None
+    assert s.last_path == "device" and s.last_device_sums is None
     if rank == 1:
         np.savez(out_path, mean=res["mean"], phi=res["phi"], acc=res["accepts"])
     dist.barrier()
@@ -131,15 +131,37 @@ def _make_sampler(chain_offset=0):
                        chain_offset=chain_offset)
 
 
+def test_device_block_sums_equal_the_host_library():
+    """ipmc_block_sums (the posterior mean's per-block sums, blocks in parallel)
+    == ipmc_host_ordered_sum from zero on each block, bit for bit: whole and
+    ragged last blocks, a row stride wider than k, div != 1, one row, no rows;
+    and shard.ordered_sum_sharded on device rows == shard.block_sum on the host."""
+    from ip_mcmc_amd import device as D
+    from ip_mcmc_amd.shard import _seq_sum, block_sum, ordered_sum_sharded
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    for n, k, stride, block, div in ((65536, 40, 40, 1024, 1.0), (5003, 257, 300, 1024, 7.0), (100, 3, 5, 16, 0.5),
+                                     (1, 1, 1, 1024, 1.0), (0, 4, 4, 8, 2.0), (4096, 40, 40, 1, 1.0)):
+        a = rng.normal(size=(n, stride)) * np.exp(rng.normal(scale=6, size=(n, 1)))
+        want = np.stack([_seq_sum(a[b : b + block, :k], np.zeros(k), div) for b in range(0, n, block)]) \
+            if n else np.zeros((0, k))
+        got = D.block_sums(torch.as_tensor(a, device=dev)[:, :k], block, div).cpu().numpy()
+        assert got.shape == want.shape and np.array_equal(got, want), (n, k, stride, block, div)
+        if n:
+            rows = torch.as_tensor(np.ascontiguousarray(a[:, :k]), device=dev)
+            assert np.array_equal(ordered_sum_sharded(rows, div=div, block=block),
+                                  block_sum(a[:, :k], div=div, block=block)), (n, k, block)
+
+
 def test_run_sharded_mean_on_the_device_equals_the_host_mean(tmp_path):
-    """gather='mean' sums the sweeps' device sums (ipmc_ordered_sum, rank by
-    rank; rank 0's sum computed by its run while the results are copied out):
-    one process and two ranks (gloo hops, both on cuda:0) give the host
-    ordered mean of the per-chain sums bit for bit."""
-    from ip_mcmc_amd.shard import _seq_sum, run_sharded
+    """gather='mean' sums the sweeps' device sums (ipmc_block_sums on each
+    rank, one all_gather): one process and two ranks (gloo, both on cuda:0)
+    give the host block_sum mean of the per-chain sums bit for bit."""
+    from ip_mcmc_amd.shard import block_sum, run_sharded
 
     one = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="mean")
-    host = _seq_sum(one["sum_u"], np.zeros(K)) / (float(one["n"]) * C_TOTAL)  # the host library's sum
+    host = block_sum(one["sum_u"]) / (float(one["n"]) * C_TOTAL)  # the host library's additions
     assert np.array_equal(one["mean"], host)
     out = str(tmp_path / "m.npz")
     mp.start_processes(_mean_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")

@@ -41,7 +41,7 @@ def test_struct_layout_matches_header():
 def test_oracle_library_loads(orc):
     from ip_mcmc_amd import _abi
 
-    assert orc.lib().orc_abi_version() == _abi.ABI_VERSION == 12
+    assert orc.lib().orc_abi_version() == _abi.ABI_VERSION == 13
 
 
 def test_struct_offsets_match_c_compiler(orc):

@@ -98,29 +98,75 @@ def test_sharded_run_equals_single_process(tmp_path, world):
     assert np.array_equal(got["mean"], ordered_mean(torch.from_numpy(U)))
 
 
-def test_ordered_mean_equals_the_sequential_loop():
-    """ipmc_host_ordered_sum is the same sequential sum as a row-by-row loop,
-    bit for bit, at 10^5 rows incl. mixed magnitudes; with div it equals the
-    loop over row/div (run_sharded's per-chain time averages)."""
-    import numpy as np
-    import torch
+def _blocked_loop(a, div=1.0, block=None):
+    """block_sum's additions as a plain loop: each block's rows from zero, then
+    the block sums in order."""
+    from ip_mcmc_amd.shard import MEAN_BLOCK
 
-    from ip_mcmc_amd.shard import _seq_sum, ordered_mean
+    block = block or MEAN_BLOCK
+    tot = np.zeros(a.shape[1])
+    for b0 in range(0, a.shape[0], block):
+        s = np.zeros(a.shape[1])
+        for row in a[b0 : b0 + block]:
+            s = s + row / div
+        tot = tot + s
+    return tot
+
+
+def test_block_sum_is_the_blocked_sequential_loop():
+    """shard.block_sum / ordered_mean (ipmc_host_ordered_sum per block, then
+    over the block sums) is the loop of the same additions, bit for bit, at
+    10^5 rows with mixed magnitudes; with div the rows are divided first; up to
+    one block it is the plain running sum."""
+    from ip_mcmc_amd.shard import MEAN_BLOCK, _seq_sum, block_sum, ordered_mean
 
     rng = np.random.default_rng(0)
     a = rng.normal(size=(100_000, 7)) * np.exp(rng.normal(scale=8, size=(100_000, 1)))
-    acc = np.zeros(7)
-    for row in a:
-        acc = acc + row
-    assert np.array_equal(ordered_mean(torch.from_numpy(a)), acc / a.shape[0])
+    assert np.array_equal(ordered_mean(torch.from_numpy(a)), _blocked_loop(a) / a.shape[0])
     assert np.array_equal(ordered_mean(a[:5]), np.cumsum(a[:5], axis=0)[-1] / 5)
-    acc = np.zeros(7)
-    for row in a[:3000]:
-        acc = acc + row / 37.0
-    assert np.array_equal(ordered_mean(a[:3000], div=37.0), acc / 3000)
-    # a split at any row continues the same sum (the rank-sequential scheme)
+    assert np.array_equal(block_sum(a[:MEAN_BLOCK]), _seq_sum(a[:MEAN_BLOCK], np.zeros(7)))
+    assert np.array_equal(ordered_mean(a[:3000], div=37.0), _blocked_loop(a[:3000], 37.0) / 3000)
+    assert np.array_equal(block_sum(a[:1000], block=16), _blocked_loop(a[:1000], block=16))
+    assert np.array_equal(block_sum(np.zeros((0, 3))), np.zeros(3))
+    # _seq_sum continues a running sum from any row (the shared blocks' rows)
     part = _seq_sum(a[:1234], np.zeros(7))
     assert np.array_equal(_seq_sum(a[1234:], part), _seq_sum(a, np.zeros(7)))
+
+
+def _osum_rows(n):
+    rng = np.random.default_rng(n)
+    return rng.normal(size=(n, 5)) * np.exp(rng.normal(scale=6, size=(n, 1)))
+
+
+def _osum_worker(rank, world, port, out_path, n_total, block, div):
+    import sys
+
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import chain_range, ordered_sum_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = chain_range(n_total, rank, world)
+    got = ordered_sum_sharded(_osum_rows(n_total)[lo:hi], div=div, block=block)
+    if rank == world - 1:
+        np.save(out_path, got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,block,div", [(3, 5003, 1024, 1.0), (8, 203, 16, 37.0), (8, 100, 64, 1.0)])
+def test_ordered_sum_sharded_equals_block_sum(tmp_path, world, n_total, block, div):
+    """The sharded sum (whole blocks summed on their rank, shared blocks' rows
+    and the block sums in one all_gather, gloo) == block_sum over all rows, bit
+    for bit: ranks spanning several blocks, blocks spanning several ranks, a
+    ragged last block, div != 1."""
+    from ip_mcmc_amd.shard import block_sum
+
+    out = str(tmp_path / "o.npy")
+    mp.start_processes(_osum_worker, args=(world, _free_port(), out, n_total, block, div), nprocs=world,
+                       start_method="spawn")
+    assert np.array_equal(np.load(out), block_sum(_osum_rows(n_total), div=div, block=block))
 
 
 # ---------------------------------------------- shard.run_sharded (product)
@@ -182,9 +228,9 @@ def test_run_sharded_equals_one_process(tmp_path, keep):
         np.testing.assert_array_equal(one["sum_u"], want["sum_u"])
 
 
-def test_run_sharded_mean_by_rank_sequential_sum(tmp_path):
+def test_run_sharded_mean_by_block_sums(tmp_path):
     """gather='mean': no per-chain sums leave their rank, yet the posterior
-    mean (a rank-sequential ordered sum) and the gathered Φ / accept counts
+    mean (fixed-order block sums) and the gathered Φ / accept counts
     equal the one-process run's bit for bit (gloo, world 3)."""
     from ip_mcmc_amd.shard import run_sharded
 

@@ -14,7 +14,7 @@ def test_torch_ops_registered_without_cpu_kernel():
     from ip_mcmc_amd import Lorenz96Operator, _abi, torch_ops
 
     ops = torch_ops.load()
-    assert ops.abi_version() == _abi.ABI_VERSION == 12
+    assert ops.abi_version() == _abi.ABI_VERSION == 13
     for name in ("pcn_sweep", "potential", "forward"):
         assert str(getattr(ops, name).default._schema).startswith(f"ipmc::{name}(")
     op = Lorenz96Operator(8, 8.0, dt=0.01, n_steps=5)
