@@ -154,6 +154,18 @@ case "$1" in
           python tools/probes/arith_kernel_probe.py r5start 40 f32 >> $O/f32_ab.jsonl || exit 1
     done
     ;;
+  s7)
+    # block-sum posterior mean (ABI 13), weak-scaling default, settled e2e legs:
+    # the whole suite, smoke, the fp32 A/B, the driver's K=20 line, a trace
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_s7.log 2>&1
+    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s7.txt 2>&1 &&
+    bash tools/sessions/r5.sh f32ab &&
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 --pmc-file profiles/r5/pmc_l96_f64.json \
+      > $O/bench_s7_k20.json 2> $O/bench_s7_k20.err &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/e2etrace_s7 -o run -- \
+      python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity > $O/e2etrace_s7.json \
+      2> $O/e2etrace_s7.err
+    ;;
   rows)
     # the configs' and the small ensembles' rows and the reference studies on the final tree
     timeout -k 10 600 python tools/config_bench.py cfg2@16384 cfg4 cfg4full cfg5 ts6 ts36 > $O/configs_final.jsonl &&
