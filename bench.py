@@ -573,8 +573,8 @@ def main():
         args.no_extra = args.no_configs = args.no_cpu = True
 
     # 2. value: MCMCSampler.run end to end through shard.run_sharded
-    # the job's result on every rank: the posterior mean (rank-sequential
-    # ordered sum, bit-identical for any N) and every chain's Φ and accept
+    # the job's result on every rank: the posterior mean (fixed-order block
+    # sums, bit-identical for any N) and every chain's Φ and accept
     # count; the per-chain states and sums stay on their rank
     gather_mode = "mean"
     if args.kernel_only:
@@ -589,9 +589,9 @@ def main():
     gather = {"ms": e2e["gather_ms"], "mode": gather_mode,
               "bytes_per_rank": int(per_rank * (3 * prob.k + 2) * 8 if gather_mode == "all" else per_rank * 16),
               "what": "every chain's Phi and accept count (all_gather_into_tensor) and the posterior mean "
-                      "(rank-sequential ordered sum of the per-chain time averages, send/recv of k doubles per rank)",
+                      "(block sums of 1 024 chains on each rank's GPU, shared blocks and block sums in one all_gather)",
               "collective": (f"all_gather_into_tensor ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
-                             + (" + rank-sequential ordered sum (send/recv)" if gather_mode == "mean" else "")
+                             + (" + block-sum all_gather" if gather_mode == "mean" else "")
                              if world > 1 else "none (one rank)"),
               "rows": int(res["phi"].shape[0]), "inside_timed_region": not args.kernel_only}
     assert np.isfinite(res["phi"]).all() and np.isfinite(res["mean"]).all()

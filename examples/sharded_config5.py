@@ -7,7 +7,7 @@ Lorenz-96 d=256, 10 000 RK4 steps per forward map, 2^20 chains by default,
 fp32 and fp64: every rank builds the same sampler with its own chain_offset
 (shard.run_sharded), runs its block of global chain ids, and the posterior
 mean -- the per-chain time averages averaged over the chains in global order
-by the rank-sequential ordered sum -- is identical for any number of GPUs.
+by fixed-order block sums -- is identical for any number of GPUs.
 Prints one JSON line per precision (rank 0): pCN steps/s over the node, the
 accept rate and the fp32-fp64 difference of the posterior means.
 """
