@@ -1,6 +1,13 @@
 // Lorenz-96 kernels, fp32 instantiations (one chain per lane group, and two
 // packed as f32x2), FMA arithmetic (REFERENCE: ipmc_l96_f32_ref.hip; one mode
 // per translation unit so they build in parallel).
+// The lane-state park (IPMC_L96_PARK, ipmc_l96.hpp) is an fp64 occupancy device
+// (two waves at 17-20 components per lane).  In this unit it changes no
+// kernel's occupancy, yet with it the compiler schedules the packed sweep's RK
+// loop differently (the same 427 instructions, reordered): 1.85 instead of
+// 1.67 ms per headline f32 sweep, three interleaved A/Bs
+// (profiles/r5/f32_ab.jsonl).  Off here: the round-4 code and schedule.
+#define IPMC_L96_PARK 0
 #include "ipmc_l96_dispatch.hpp"
 
 namespace ipmc {
