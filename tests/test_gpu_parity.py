@@ -196,8 +196,17 @@ def test_sweep_l96_bit_exact_every_layout(dev, orc, dtype, cpl, K, lanes):
     131 chains so the packed fp32 layout has a phantom partner in its last pair."""
     from ip_mcmc_amd import Lorenz96Operator
 
+    from ip_mcmc_amd._lib import UnsupportedOnDevice
+
     if (dtype == torch.float64 or cpl == 2) and K // lanes > 20:
-        pytest.skip("no 8-byte-storage instantiation with more than 20 components per lane")
+        # no 8-byte-storage kernel holds more than 20 components per lane: the
+        # library refuses the layout by name (ipmc_last_error) instead of
+        # running another one
+        op = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=60)
+        U0, phi0, y, ginv, sq = _problem(op, 131, dtype, orc, seed=K)
+        with pytest.raises(UnsupportedOnDevice, match=f"dim={K} lanes_per_chain={lanes}"):
+            _sweep_device(op, U0, phi0, y, ginv, sq, 0.25, 77, 5, 6, dtype, dev, lanes=lanes, cpl=cpl)
+        return
     for arith in ("fma", "reference"):
         op = Lorenz96Operator(K, 8.0, dt=0.005, n_steps=60, arith=arith)
         U0, phi0, y, ginv, sq = _problem(op, 131, dtype, orc, seed=K)
