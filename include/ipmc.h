@@ -250,8 +250,8 @@ int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars,
                  int64_t* out, void* stream);
 
 /* (ABI 12) acc[j] = (((acc[j] + rows[0][j]/div) + rows[1][j]/div) + ...) for j < k over the n_rows rows
-   (row r at rows + r*row_stride doubles), strictly in row order -- the chain-ordered sum of the many-chain
-   posterior mean (shard.ordered_sum_sharded), equal bit for bit to ipmc_host_ordered_sum (ipmc_host.h);
+   (row r at rows + r*row_stride doubles), strictly in row order -- one dependent chain of adds per column
+   (the posterior mean uses ipmc_block_sums since ABI 13), equal bit for bit to ipmc_host_ordered_sum (ipmc_host.h);
    div == 1 adds the rows as they are.  Device pointers; acc [k] in/out. */
 int ipmc_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div, double* acc,
                      void* stream);
