@@ -168,3 +168,37 @@ def test_run_sharded_mean_on_the_device_equals_the_host_mean(tmp_path):
     got = np.load(out)
     assert np.array_equal(got["mean"], one["mean"])
     assert np.array_equal(got["phi"], one["phi"]) and np.array_equal(got["acc"], one["accepts"])
+
+
+def _osum_rows(n):
+    rng = np.random.default_rng(n)
+    return rng.normal(size=(n, 7)) * np.exp(rng.normal(scale=6, size=(n, 1)))
+
+
+def _osum_worker(rank, world, port, out_path, n_total, div):
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import chain_range, ordered_sum_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = chain_range(n_total, rank, world)
+    rows = torch.as_tensor(_osum_rows(n_total)[lo:hi], device=torch.device("cuda", 0))
+    got = ordered_sum_sharded(rows, div=div)
+    if rank == world - 1:
+        np.save(out_path, got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,div", [(2, 5003, 1.0), (3, 4100, 3.0)])
+def test_sharded_block_sums_on_the_device_equal_block_sum(tmp_path, world, n_total, div):
+    """Device rows over ranks (gloo, all on cuda:0): each rank's whole blocks
+    by ipmc_block_sums, the blocks it shares with a neighbour as raw rows, one
+    all_gather -- block_sum over all rows on the host, bit for bit."""
+    from ip_mcmc_amd.shard import block_sum
+
+    out = str(tmp_path / "o.npy")
+    mp.start_processes(_osum_worker, args=(world, _free_port(), out, n_total, div), nprocs=world,
+                       start_method="spawn")
+    assert np.array_equal(np.load(out), block_sum(_osum_rows(n_total), div=div))
