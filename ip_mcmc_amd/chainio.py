@@ -54,10 +54,16 @@ class NpySampleSink:
 
 
 class ChainState:
-    """Everything needed to continue a run exactly (host numpy arrays)."""
+    """Everything needed to continue a run exactly (host numpy arrays).  A run
+    with results='device' leaves the chain states in HBM: ``u`` is then copied
+    to the host on first access, and ``u_device`` is the device tensor (what a
+    resumed run starts from, without a round trip)."""
 
     def __init__(self, u, phi, accepts, calls, seed, step, proposer_i, dtype, chain_offset=None, accept_kind=None):
-        self.u = np.asarray(u)
+        if hasattr(u, "is_cuda") and u.is_cuda:
+            self.u_device, self._u = u, None
+        else:
+            self.u_device, self._u = None, np.asarray(u)
         self.phi = np.asarray(phi)
         self.accepts = np.asarray(accepts)
         self.calls = None if calls is None else np.asarray(calls)
@@ -72,8 +78,18 @@ class ChainState:
         self.accept_kind = None if accept_kind is None else str(accept_kind)
 
     @property
+    def u(self):
+        if self._u is None:
+            self._u = self.u_device.detach().cpu().numpy()
+        return self._u
+
+    @u.setter
+    def u(self, value):
+        self.u_device, self._u = None, np.asarray(value)
+
+    @property
     def n_chains(self):
-        return self.u.shape[0]
+        return (self.u_device if self._u is None else self._u).shape[0]
 
 
 def save_state(path, state):

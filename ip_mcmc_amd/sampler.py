@@ -160,11 +160,18 @@ class MCMCSampler:
 
     # ------------------------------------------------------------------ run
     def run(self, u_0, n_samples, burn_in=1000, sample_interval=200, keep="samples", sample_file=None,
-            flush_every=None):
+            flush_every=None, results="host"):
         """Run the chain(s).  keep='samples' returns the samples like the
         reference; keep='moments' returns a dict of per-chain sums of u and u²
         over every post-burn-in step (no sample array); keep='last' returns
         the final states (C, k).
+
+        results='device' (keep='moments' or 'last', device path) leaves the
+        per-chain results in HBM: the sums / last states come back as device
+        tensors and the checkpoint's states stay on the device (ChainState.u is
+        copied to the host on first access); only Φ and the counters are
+        copied.  u_0 may then be a device tensor too, so a run starts and ends
+        in HBM.  The host tier always returns host arrays.
 
         u_0 may be a ChainState (``checkpoint()`` / ``chainio.load_state``):
         the run then continues those chains exactly (same Φ cache, Philox
@@ -173,6 +180,11 @@ class MCMCSampler:
         ``flush_every`` samples) and returns it memory-mapped."""
         if keep not in ("samples", "moments", "last"):
             raise ValueError("keep must be 'samples', 'moments' or 'last'")
+        if results not in ("host", "device"):
+            raise ValueError("results must be 'host' or 'device'")
+        if results == "device" and keep == "samples":
+            raise ValueError("results='device' keeps keep='moments' or 'last' in HBM")
+        on_dev = results == "device"
         t_entry = time.perf_counter()
         self.last_device_sums = None
         try:
@@ -190,10 +202,11 @@ class MCMCSampler:
         k = plan.G.k
         resume = isinstance(u_0, ChainState)
         if resume:
-            if u_0.u.shape[1] != k:
-                raise ValueError(f"ChainState has k={u_0.u.shape[1]}, forward map k={k}")
+            u_src = u_0.u_device if u_0.u_device is not None else u_0.u
+            if u_src.shape[1] != k:
+                raise ValueError(f"ChainState has k={u_src.shape[1]}, forward map k={k}")
             single = False
-            U = dev.to_device(u_0.u, td, device).clone()
+            U = dev.to_device(u_src, td, device).clone()
         elif isinstance(u_0, torch.Tensor):
             single = u_0.dim() <= 1
             U = u_0.reshape(-1, k).to(device=device, dtype=td).clone().contiguous()
@@ -439,8 +452,11 @@ class MCMCSampler:
         # the chain state (u, Φ, counters) to page-locked host memory on the
         # sweep stream, queued before the wait: a pageable copy of u alone was
         # ~2-4 ms after the sweeps at the headline size (21 MB)
-        state_host = [_pinned_copy(t) for t in (U, phi, accepts, calls) if t is not None]
-        sums_host = None if sums is None else [_pinned_copy(t) for t in sums]
+        # (results='device': the states and sums stay in HBM; Φ and the counters,
+        # 16 B per chain, still come back for the checkpoint and the counters)
+        state_host = [None if on_dev else _pinned_copy(U)] + [_pinned_copy(t) for t in (phi, accepts, calls)
+                                                              if t is not None]
+        sums_host = None if (sums is None or on_dev) else [_pinned_copy(t) for t in sums]
         torch.cuda.synchronize(device)
         self.last_run_seconds = time.perf_counter() - t0
 
@@ -449,7 +465,8 @@ class MCMCSampler:
         if hasattr(plan.proposer, "i"):
             plan.proposer.i = prop_i
 
-        u_np, phi_np, acc_np = (t.numpy() for t in state_host[:3])
+        u_np = U if on_dev else state_host[0].numpy()
+        phi_np, acc_np = (t.numpy() for t in state_host[1:3])
         calls_np = state_host[3].numpy() if calls is not None else None
         for ca in plan.counted_outer:
             _bump(ca, np.full(n_chains, total, dtype=np.int64), acc_np, single)
@@ -486,11 +503,12 @@ class MCMCSampler:
         self.last_device_sums = sums if (keep == "moments" and self.keep_device_sums) else None
         if keep == "moments":
             n_post = n_samples * sample_interval
-            res = {"sum_u": sums_host[0].numpy(), "sum_u2": sums_host[1].numpy(), "n": n_post}
+            su, su2 = (sums[0], sums[1]) if on_dev else (sums_host[0].numpy(), sums_host[1].numpy())
+            res = {"sum_u": su, "sum_u2": su2, "n": n_post}
             if single:
                 res = {"sum_u": res["sum_u"][0], "sum_u2": res["sum_u2"][0], "n": n_post}
             return res
-        last = np.array(u_np, dtype=np.float64)
+        last = U.double() if on_dev else np.array(u_np, dtype=np.float64)
         return last[0] if single else last
 
     def checkpoint(self):

@@ -202,7 +202,7 @@ def _comm_device(group):
 
 
 def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200, keep="moments", group=None,
-                sample_file=None, gather="all"):
+                sample_file=None, gather="all", results="host"):
     """MCMCSampler.run over the chains of every rank of a node, one process per GPU.
 
     make_sampler(chain_offset=...) builds this rank's sampler (the same
@@ -232,6 +232,10 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     and forms "mean" by ordered_sum_sharded (block sums), for ensembles
     whose per-chain arrays are too large to copy to every rank (config 5:
     2^20 chains x 256); "u", "sum_u", "sum_u2" are then this rank's rows only.
+    results="device" (with gather="mean"): the rank's per-chain results stay
+    in HBM ("u", "sum_u", "sum_u2" are this rank's device tensors; u_0 may be
+    a device tensor) -- a job that starts and ends in HBM, no PCIe on the data
+    path; "mean", "phi" and "accepts" are host arrays as before.
     With one rank (no process group) it is a plain run()."""
     import time
 
@@ -243,6 +247,8 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         raise ValueError("gather must be 'all' or 'mean'")
     if gather == "mean" and keep != "moments":
         raise ValueError("gather='mean' needs keep='moments'")
+    if results == "device" and gather != "mean":
+        raise ValueError("results='device' needs gather='mean' (the per-chain rows stay on their rank)")
     if len(np.shape(u_0)) != 2:
         raise ValueError("run_sharded needs u_0 of shape (chains, k)")
     n_total = int(np.shape(u_0)[0])
@@ -253,15 +259,16 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     # gather="mean": the posterior mean's block sums run on the device sums the
     # sweeps left (MCMCSampler.last_device_sums) when the run was a device run
     sampler.keep_device_sums = gather == "mean"
-    local_u0 = np.asarray(u_0[lo:hi], dtype=np.float64)
+    local_u0 = u_0[lo:hi] if isinstance(u_0, torch.Tensor) else np.asarray(u_0[lo:hi], dtype=np.float64)
     sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
     t0 = time.perf_counter()
     res = sampler.run(local_u0, n_samples, burn_in=burn_in, sample_interval=sample_interval, keep=keep,
-                      sample_file=sf)
+                      sample_file=sf, results=results)
     run_s = time.perf_counter() - t0
     st = sampler.state
     k = local_u0.shape[1]
-    cols = [np.asarray(st.u, dtype=np.float64).reshape(hi - lo, k),
+    u_rows = st.u_device if st.u_device is not None else np.asarray(st.u, dtype=np.float64).reshape(hi - lo, k)
+    cols = [u_rows,
             np.asarray(st.phi, dtype=np.float64).reshape(hi - lo, 1),
             np.asarray(st.accepts, dtype=np.float64).reshape(hi - lo, 1)]  # counts < 2^53: exact
     if gather == "mean":

@@ -63,6 +63,9 @@ def test_bench_gpus_2_launches_its_own_ranks():
     # value is the end-to-end run; the kernel leg is beside it
     assert line["value"] == ex["run_e2e_moments"]["pcn_steps_per_s"] and ex["kernel_pcn_steps_per_s"] > 0
     assert abs(line["ms_per_step"] * line["steps"] / 1e3 - ex["run_e2e_moments"]["wall_s"]) < 1e-9
+    # value's data in HBM; the host-buffer run (PCIe included) beside it
+    assert ex["run_e2e_moments"]["data_in_hbm"] and not ex["run_e2e_pcie"]["data_in_hbm"]
+    assert ex["run_e2e_pcie"]["pcn_steps_per_s"] > 0
     assert ex["mixing_posterior"]["total_chains"] == 131072 and ex["mixing_posterior"]["pcn_steps_per_s"] > 0
     # REFERENCE arith end to end beside value; the paired streams run at N = 1 only
     assert line["parity"]["reference_arith_value"] > 0 and "paired_identical_accept_frac" not in line["parity"]

@@ -202,3 +202,37 @@ def test_sharded_block_sums_on_the_device_equal_block_sum(tmp_path, world, n_tot
     mp.start_processes(_osum_worker, args=(world, _free_port(), out, n_total, div), nprocs=world,
                        start_method="spawn")
     assert np.array_equal(np.load(out), block_sum(_osum_rows(n_total), div=div))
+
+
+def test_results_on_the_device_equal_the_host_results():
+    """results='device': a run that starts (u_0 a device tensor) and ends in
+    HBM gives the host run's sums, states, Φ and counters bit for bit; the
+    checkpoint's states stay on the device and a resumed run from it equals
+    one resumed from the host state; run_sharded's gather='mean' keeps the
+    rank's rows on the device and forms the same mean."""
+    from ip_mcmc_amd.shard import run_sharded
+
+    dev = torch.device("cuda", 0)
+    u0 = _u0()
+    a, b = _make_sampler(), _make_sampler()
+    rh = a.run(u0, n_samples=2, burn_in=0, sample_interval=3, keep="moments")
+    rd = b.run(torch.as_tensor(u0, device=dev), n_samples=2, burn_in=0, sample_interval=3, keep="moments",
+               results="device")
+    assert rd["sum_u"].is_cuda and b.state.u_device is not None
+    assert np.array_equal(rd["sum_u"].cpu().numpy(), rh["sum_u"])
+    assert np.array_equal(rd["sum_u2"].cpu().numpy(), rh["sum_u2"])
+    assert np.array_equal(b.state.phi, a.state.phi) and np.array_equal(b.state.accepts, a.state.accepts)
+    assert np.array_equal(b.state.u, a.state.u)  # copied to the host on first access
+    la = a.run(a.checkpoint(), n_samples=1, burn_in=0, sample_interval=2, keep="last")
+    lb = b.run(b.checkpoint(), n_samples=1, burn_in=0, sample_interval=2, keep="last", results="device")
+    assert lb.is_cuda and np.array_equal(lb.cpu().numpy(), la)
+    with pytest.raises(ValueError):
+        b.run(u0, n_samples=1, burn_in=0, sample_interval=1, keep="samples", results="device")
+    one = run_sharded(_make_sampler, u0, n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="mean")
+    dd = run_sharded(_make_sampler, torch.as_tensor(u0, device=dev), n_samples=1, burn_in=0, sample_interval=6,
+                     keep="moments", gather="mean", results="device")
+    assert dd["u"].is_cuda and dd["sum_u"].is_cuda
+    for key in ("mean", "phi", "accepts"):
+        assert np.array_equal(dd[key], one[key]), key
+    assert np.array_equal(dd["u"].cpu().numpy(), one["u"]) and np.array_equal(dd["sum_u"].cpu().numpy(),
+                                                                               one["sum_u"])
