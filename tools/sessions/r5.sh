@@ -166,6 +166,14 @@ case "$1" in
       python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity > $O/e2etrace_s7.json \
       2> $O/e2etrace_s7.err
     ;;
+  s9)
+    # results='device' (value with the data in HBM), block sums over ranks on
+    # the device: the sampler / shard / N-rank tests, the driver's K=20 line
+    tests_ok timeout -k 10 900 $PYT tests/test_gpu_shard.py tests/test_gpu_bench_dist.py tests/test_gpu_run.py \
+      tests/test_gpu_sampler_edges.py tests/test_gpu_hostloop.py > $O/pytest_s9.log 2>&1
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 --pmc-file profiles/r5/pmc_l96_f64.json \
+      > $O/bench_s9_k20.json 2> $O/bench_s9_k20.err
+    ;;
   rows)
     # the configs' and the small ensembles' rows and the reference studies on the final tree
     timeout -k 10 600 python tools/config_bench.py cfg2@16384 cfg4 cfg4full cfg5 ts6 ts36 > $O/configs_final.jsonl &&
