@@ -508,7 +508,7 @@ class MCMCSampler:
             if single:
                 res = {"sum_u": res["sum_u"][0], "sum_u2": res["sum_u2"][0], "n": n_post}
             return res
-        last = U.double() if on_dev else np.array(u_np, dtype=np.float64)
+        last = U.to(torch.float64, copy=True) if on_dev else np.array(u_np, dtype=np.float64)
         return last[0] if single else last
 
     def checkpoint(self):
