@@ -94,14 +94,16 @@ def _seq_sum(a, acc, div=1.0):
     return acc.reshape(a.shape[1:])
 
 
-def _segments(lo, hi, block):
-    """[lo, hi) cut at the multiples of `block`: (start, stop, whole block?)."""
-    segs, s = [], lo
-    while s < hi:
-        e = min(hi, (s // block + 1) * block)
-        segs.append((s, e, e - s == block))
-        s = e
-    return segs
+def _split(lo, hi, block):
+    """[lo, hi) against the blocks of `block` rows: (head, (b0, b1), tail) --
+    the whole blocks b0..b1-1 and the rows (start, stop) before and after them
+    that share a block with other ranks (None where there are none)."""
+    fb, lb = -(-lo // block), hi // block
+    if fb > lb:  # inside one block, no boundary in between
+        return ((lo, hi) if hi > lo else None), (0, 0), None
+    head = (lo, fb * block) if lo < fb * block else None
+    tail = (lb * block, hi) if lb * block < hi else None
+    return head, (fb, lb), tail
 
 
 def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
@@ -134,10 +136,9 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
         counts = [n_local]
     los = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     lo = int(los[rank])
-    segs = _segments(lo, lo + n_local, block)
-    whole = [(s0, e0) for s0, e0, w in segs if w]
-    if whole:  # a rank's whole blocks are consecutive
-        f0, f1 = whole[0][0] - lo, whole[-1][1] - lo
+    head, (b0, b1), tail = _split(lo, lo + n_local, block)
+    if b1 > b0:  # this rank's whole blocks, in one call
+        f0, f1 = b0 * block - lo, b1 * block - lo
         if on_dev:
             from . import device as D
 
@@ -146,15 +147,16 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
             F = _host_block_sums(rows[f0:f1], div, block)
     else:
         F = np.zeros((0, k))
-    shared = [rows[s0 - lo : e0 - lo] for s0, e0, w in segs if not w]
+    shared = [rows[seg[0] - lo : seg[1] - lo] for seg in (head, tail) if seg is not None]
     shared = [p.cpu().numpy() if on_dev else p for p in shared]
     mine = np.concatenate([F.reshape(-1)] + [p.reshape(-1) for p in shared]) if (len(F) or shared) else np.zeros(0)
+
+    def size(r):  # every rank's contribution, known from the counts alone
+        h, (c0, c1), t = _split(int(los[r]), int(los[r + 1]), block)
+        return ((c1 - c0) + sum(seg[1] - seg[0] for seg in (h, t) if seg is not None)) * k
+
     if world > 1:
-        sizes = []
-        for r in range(world):
-            sr = _segments(int(los[r]), int(los[r + 1]), block)
-            sizes.append(sum(1 if w else (e0 - s0) for s0, e0, w in sr) * k)
-        per = max(max(sizes), 1)
+        per = max(max(size(r) for r in range(world)), 1)
         buf = torch.zeros(per, dtype=torch.float64, device=dev)
         buf[: mine.size] = torch.from_numpy(mine).to(dev)
         allb = torch.empty(per * world, dtype=torch.float64, device=dev)
@@ -167,18 +169,13 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
     sums = np.zeros((-(-n_total // block), k), dtype=np.float64)
     pieces = {}
     for r in range(world):
-        off = 0
-        sr = _segments(int(los[r]), int(los[r + 1]), block)
-        nw = sum(1 for _, _, w in sr if w)
-        Fr = parts[r][: nw * k].reshape(nw, k)
-        off, i = nw * k, 0
-        for s0, e0, w in sr:
-            if w:
-                sums[s0 // block] = Fr[i]
-                i += 1
-            else:
-                m = (e0 - s0) * k
-                pieces.setdefault(s0 // block, []).append(parts[r][off : off + m].reshape(e0 - s0, k))
+        h, (c0, c1), t = _split(int(los[r]), int(los[r + 1]), block)
+        sums[c0:c1] = parts[r][: (c1 - c0) * k].reshape(c1 - c0, k)
+        off = (c1 - c0) * k
+        for seg in (h, t):  # head rows, then tail rows: global row order
+            if seg is not None:
+                m = (seg[1] - seg[0]) * k
+                pieces.setdefault(seg[0] // block, []).append(parts[r][off : off + m].reshape(seg[1] - seg[0], k))
                 off += m
     for b, pc in pieces.items():  # a block over several ranks: its rows in rank order, from zero
         sums[b] = _seq_sum(np.concatenate(pc), np.zeros(k), div)

@@ -133,6 +133,29 @@ def test_block_sum_is_the_blocked_sequential_loop():
     assert np.array_equal(_seq_sum(a[1234:], part), _seq_sum(a, np.zeros(7)))
 
 
+def test_split_partitions_a_range_at_block_boundaries():
+    """shard._split: head + whole blocks + tail cover [lo, hi) in order; the
+    whole blocks are exactly the blocks inside the range; head and tail each
+    lie in one block that the range does not cover whole."""
+    from ip_mcmc_amd.shard import _split
+
+    for block in (1, 3, 16):
+        for lo in range(0, 40):
+            for hi in range(lo, 60):
+                head, (b0, b1), tail = _split(lo, hi, block)
+                rows = []
+                if head is not None:
+                    assert head[0] // block == (head[1] - 1) // block and head[1] - head[0] < block
+                    rows += list(range(*head))
+                rows += list(range(b0 * block, b1 * block))
+                if tail is not None:
+                    assert tail[0] // block == (tail[1] - 1) // block and tail[1] - tail[0] < block
+                    rows += list(range(*tail))
+                assert rows == list(range(lo, hi)), (lo, hi, block)
+                inside = [b for b in range(0, 60 // block + 2) if lo <= b * block and (b + 1) * block <= hi]
+                assert list(range(b0, b1)) == inside, (lo, hi, block)
+
+
 def _osum_rows(n):
     rng = np.random.default_rng(n)
     return rng.normal(size=(n, 5)) * np.exp(rng.normal(scale=6, size=(n, 1)))
