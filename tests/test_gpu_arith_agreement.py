@@ -64,3 +64,30 @@ def test_fma_and_reference_posteriors_agree_at_the_headline_shape():
     assert abs(r["mean_z2"] - 1) < BAND, r
     assert abs(r["t2_over_d"] - 1) < BAND, r
     assert r["paired_identical_accept_counts"] >= PAIRED_MIN, r
+
+
+# the reference's own noise level r = 0.5 (lorenz_mcmc.py:92): the chains stick
+# for thousands of steps (R-hat 2.1 after 2 400), so 50 000 pCN steps per chain
+# (R-hat 1.05; profiles/r5/posterior_r05_long.jsonl), unpaired
+RUN_R05 = (8192, 40, 1250, 0.2, 0.5)
+
+
+def test_fma_and_reference_posteriors_agree_at_the_references_noise_level():
+    import torch
+
+    import posterior_agreement as PA
+
+    assert torch.cuda.is_available()
+    chains, n_seg, seg_len, beta, noise_r = RUN_R05
+    r = PA.measure("arith", chains, n_seg, seg_len, beta, noise_r, paired=False)
+    print(r)
+    assert r["d"] == D and r["noise_r"] == 0.5 and r["pcn_steps"] == 50000
+    assert "burn_in_capped_from" not in r, r
+    for arm in ("fma_float64", "reference_float64"):
+        a = r[arm]
+        assert 0.02 < a["accept_rate"] < 0.98, a
+        assert a["half_z_max"] < Z_MAX and a["half_var_z_max"] < Z_MAX, a
+        assert a["rhat_max"] < 1.2, a
+    assert r["max_z"] < Z_MAX, r
+    assert abs(r["mean_z2"] - 1) < BAND, r
+    assert abs(r["t2_over_d"] - 1) < BAND, r
