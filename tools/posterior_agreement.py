@@ -121,6 +121,8 @@ def blocks(d, n_rk, y, gamma, x0, arith, dtype, seed, u0, n_seg, seg_len):
         wall += time.perf_counter() - t0
         B[:, j] = mom["sum_u"] / mom["n"]
         state = s.checkpoint()
+        print(f"[posterior_agreement] {arith} {np.dtype(dtype).name} block {j + 1}/{n_seg} "
+              f"({wall:.1f} s)", file=sys.stderr, flush=True)  # progress: long runs stay visibly alive
     return B, np.asarray(state.accepts, dtype=np.int64), wall
 
 
