@@ -63,8 +63,33 @@ from ip_mcmc_amd._lib import call  # noqa: E402
 ITEM = {"f64": 8, "f32": 4}
 PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}  # MI355X vector (spec), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
-CHAINS_PER_GPU = 65536  # cfg3's metric ensemble (the weak-scaling share)
+METRIC_CHAINS = 65536  # cfg3's metric ensemble: 65 536 chains over the node (BASELINE.json "metric")
 METRIC = "pCN steps/sec (whole node), Lorenz-96 d=40 T=2000, 65 536 chains"
+WORKLOAD_CHAINS = {"cfg3": METRIC_CHAINS, "cfg4": 16384, "cfg5": 1 << 20}  # per node, as BASELINE states them
+
+
+def ensemble(workload, world, chains=None, scaling=None):
+    """(scaling, total chains over the node) of a bench run.  Every BASELINE
+    workload states its ensemble per node (cfg3's metric: 65 536 chains over
+    the whole node), so the default is strong scaling: the node's ensemble
+    split over the N GPUs (8 192 chains per GPU at N = 8).  --scaling weak
+    runs --chains (default: the workload's ensemble) on EVERY GPU; cfg3's line
+    carries that figure beside value (extra.weak_scaling)."""
+    scaling = scaling or "strong"
+    per = int(chains or WORKLOAD_CHAINS[workload])
+    return scaling, per * (world if scaling == "weak" else 1)
+
+
+def metric_name(workload, prob_name, total_chains):
+    """The line's metric: BASELINE's own string exactly when the run is its
+    configuration (cfg3 with 65 536 chains over the node), else the same form
+    naming the chains actually run, so a line never quotes one ensemble's
+    name for another's throughput."""
+    grouped = f"{total_chains:,}".replace(",", " ")
+    if workload == "cfg3":
+        return METRIC if total_chains == METRIC_CHAINS else \
+            f"pCN steps/sec (whole node), Lorenz-96 d=40 T=2000, {grouped} chains"
+    return f"pCN steps/sec (whole node), {prob_name}, {total_chains} chains"
 
 
 class Problem:
@@ -349,13 +374,18 @@ def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="a
     gathered result."""
     from ip_mcmc_amd.shard import run_sharded
 
+    from ip_mcmc_amd.shard import chain_range, world_info
+
     make = sampler_factory(prob, dtype_np, dev, seed)
     resident = resident and gather == "mean"
     kw = {"results": "device"} if resident else {}
+    # only this rank's block of u_0 (run_sharded(n_total=...)): no rank holds the node's ensemble
+    lo, hi = chain_range(total_chains, world_info()[0], world)
     if resident:  # in HBM before the timed region starts
-        u0 = torch.zeros((total_chains, prob.k), dtype=torch.float64, device=dev)
+        u0 = torch.zeros((hi - lo, prob.k), dtype=torch.float64, device=dev)
     else:
-        u0 = np.full((total_chains, prob.k), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch)
+        u0 = np.full((hi - lo, prob.k), 0.0)  # written, i.e. resident (np.zeros maps its pages on first touch)
+    kw["n_total"] = total_chains
     if warmup > 0:
         run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=warmup, keep="moments", gather=gather, **kw)
     if settle is not None:
@@ -373,7 +403,7 @@ def timed_run(prob, dtype_np, dev, total_chains, steps, warmup, world, gather="a
     assert smp.last_path == "device" and smp.state.steps_this_run == steps
     tm = smp.last_run_timing
     rec = {"pcn_steps_per_s": total_chains * steps / el, "wall_s": el, "ms_per_step": el / steps * 1e3,
-           "steps": steps, "total_chains": total_chains, "chains_per_gpu": total_chains // world,
+           "steps": steps, "total_chains": total_chains, "chains_per_gpu": hi - lo, "u0_rows_per_rank": hi - lo,
            "accept_rate": float(res["accepts"].sum()) / (total_chains * steps),
            "run_seconds_rank0": res["run_seconds"], "gather_ms": res["gather_seconds"] * 1e3,
            "setup_ms": tm["setup_s"] * 1e3, "phi0_gpu_ms": tm["phi0_gpu_ms"], "sweeps_gpu_ms": tm["sweeps_gpu_ms"],
@@ -432,7 +462,28 @@ def config_line(key, dev, world, steps=None, warmup=None, chains=None):
         out["tflops_f32"] = total * prob.flop * st / rec32["wall_s"] / 1e12
         out["f32_over_f64"] = rec32["pcn_steps_per_s"] / rec64["pcn_steps_per_s"]
         out["posterior_mean_max_abs_diff_f32_f64"] = float(np.max(np.abs(r32["mean"] - r64["mean"])))
+        tf_ref = out["tflops_reference_f64"]
+        out["arith_parity"] = {
+            "bit_exact_arith": "reference",
+            "bit_exact_pcn_steps_per_s": recr["pcn_steps_per_s"],
+            "fma_pcn_steps_per_s": rec64["pcn_steps_per_s"],
+            "fma_paired_identical_accept_frac": None,  # filled from parity.cfg5 when the paired run is in the line
+            "tflops_reference_f64": tf_ref,
+            "reference_frac_of_peak": tf_ref / PEAK_TFLOPS["f64"],
+            "reference_op_ceiling_frac": CFG5_REFERENCE_CEILING,
+            "note": "at config 5 the bit-exact accept streams (GPU == oracle == the reference's operation order, "
+                    "lorenz.py:77-81) are REFERENCE arith's: its rate is bit_exact_pcn_steps_per_s.  The FMA chains "
+                    "(fma_pcn_steps_per_s, the faster rate) are not the reference's chains: 50 time units of chaos "
+                    "part the paired streams at the first steps (fma_paired_identical_accept_frac); their claim is "
+                    "the stated stationary tolerance.  REFERENCE arith issues 32 FP64 ops (no FMA) per component "
+                    "and RK4 step plus 24 DPP moves per 16 components (the d=256 kernel's loop, hipcc -S): "
+                    "30 FLOP / (2 x 33.5 slots) = 0.448 of the FP64 peak is its op-mix ceiling"}
     return out
+
+
+# REFERENCE arith's op-mix ceiling at d=256 on 16 lanes: 30 FLOP per component
+# and RK4 step in 32 unfused FP64 ops + 24 DPP moves / 16 components
+CFG5_REFERENCE_CEILING = 30 / (2 * (32 + 24 / 16))
 
 
 def cpu_baseline(prob, dtype_np, budget_s=15.0):
@@ -558,20 +609,18 @@ def main():
     prob = make_problem(args.workload)
     steps = args.steps if args.steps is not None else prob.steps
     warmup = args.warmup if args.warmup is not None else prob.warmup
-    chains = args.chains or prob.chains
-    if args.scaling is None:
-        args.scaling = "weak" if args.workload == "cfg3" else "strong"
-    total_chains = chains * (world if args.scaling == "weak" else 1)
-    if total_chains % world:
-        raise SystemExit("--scaling strong needs --chains divisible by the number of GPUs")
-    per_rank = total_chains // world
+    args.scaling, total_chains = ensemble(args.workload, world, args.chains, args.scaling)
+    from ip_mcmc_amd.shard import chain_range
+
+    lo_rank, hi_rank = chain_range(total_chains, rank, world)  # this rank's global chain ids
+    per_rank = hi_rank - lo_rank
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
     ndt = np.float64 if args.dtype == "f64" else np.float32
 
     # 1. kernel leg: device-resident sweeps, HIP events (the roofline's kernel time)
     # (a launch never exceeds the timed steps: the plan reported is the one timed)
     per_launch = min(args.steps_per_launch or auto_per_launch(per_rank), max(1, steps))
-    w = Workload(prob, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch,
+    w = Workload(prob, per_rank, lo_rank, tdt, dev, args.lanes, per_launch=per_launch,
                  spec_width=args.spec_width)
     log(f"kernel leg: {steps} pCN steps ({args.dtype}, {per_rank} chains/GPU, {per_launch} steps/launch, "
         f"lanes={w.lanes}, spec_width={w.spec_width})")
@@ -645,7 +694,7 @@ def main():
         xs = min(steps, 40) if per_launch == 1 else steps
         other = torch.float32 if tdt == torch.float64 else torch.float64
         key = "f32" if other == torch.float32 else "f64"
-        w2 = Workload(prob, per_rank, rank * per_rank, other, dev, args.lanes, per_launch=per_launch)
+        w2 = Workload(prob, per_rank, lo_rank, other, dev, args.lanes, per_launch=per_launch)
         el2, k2 = timed(w2, xs, 2, world)
         log(f"{key}: kernel {k2:.3f} ms/launch")
         extra[f"{key}_kernel_pcn_steps_per_s"] = total_chains * xs / el2
@@ -658,7 +707,7 @@ def main():
         # the reference's operation order (no FMA in the forward map): the
         # arithmetic whose accept streams are pinned to the reference fixtures
         pref = prob.reference_arith()
-        w3 = Workload(pref, per_rank, rank * per_rank, tdt, dev, args.lanes, per_launch=per_launch)
+        w3 = Workload(pref, per_rank, lo_rank, tdt, dev, args.lanes, per_launch=per_launch)
         xr = min(xs, 20) if per_launch == 1 else xs
         el3, k3 = timed(w3, xr, 2, world)
         log(f"reference arith ({args.dtype}): kernel {k3:.3f} ms/launch")
@@ -681,17 +730,22 @@ def main():
                                          accept_rate_value=accept_rate)
         if world > 1:  # the other scaling beside the line: 65 536 chains per GPU / over the node
             other_s = "strong" if args.scaling == "weak" else "weak"
-            n_other = CHAINS_PER_GPU * (world if other_s == "weak" else 1)
+            n_other = ensemble(args.workload, world, None, other_s)[1]
             wk, _ = timed_run(prob, ndt, dev, n_other, steps, 2, world, gather=gather_mode, settle=settle)
             extra[f"{other_s}_scaling"] = {"pcn_steps_per_s": wk["pcn_steps_per_s"], "total_chains": n_other,
-                                           "chains_per_gpu": n_other // world, "ms_per_step": wk["ms_per_step"],
-                                           "steps": wk["steps"], "timed": "run_sharded end to end, keep='moments'"}
-        extra["run_e2e_samples"] = e2e_samples(prob, per_rank, rank * per_rank, ndt, dev, world)
+                                           "chains_per_gpu": wk["chains_per_gpu"], "ms_per_step": wk["ms_per_step"],
+                                           "steps": wk["steps"], "timed": "run_sharded end to end, keep='moments'",
+                                           "metric": metric_name(args.workload, prob.name, n_other)}
+        extra["run_e2e_samples"] = e2e_samples(prob, per_rank, lo_rank, ndt, dev, world)
     if not args.no_configs and args.workload == "cfg3":
         cfgs = {}
         for key in ("cfg4", "cfg5"):
             log(f"extra.configs: {key} end to end")
             cfgs[key] = config_line(key, dev, world)
+        if "cfg5" in parity and "arith_parity" in cfgs["cfg5"]:
+            cfgs["cfg5"]["arith_parity"]["fma_paired_identical_accept_frac"] = \
+                parity["cfg5"]["identical_accept_stream_frac"]
+            cfgs["cfg5"]["arith_parity"]["fma_paired"] = {k: parity["cfg5"][k] for k in ("chains", "steps")}
         extra["configs"] = cfgs
     del settle, w
 
@@ -717,8 +771,7 @@ def main():
     if rank == 0:
         item = ITEM[args.dtype]
         line = {
-            "metric": METRIC if args.workload == "cfg3" else f"pCN steps/sec (whole node), {prob.name}, "
-                                                             f"{total_chains} chains",
+            "metric": metric_name(args.workload, prob.name, total_chains),
             "value": value,
             "unit": "pCN steps/s",
             "n_gpus": world,

@@ -198,15 +198,49 @@ def _comm_device(group):
     return torch.device("cpu")
 
 
+def local_start(u_0, n_total, rank, world):
+    """This rank's block of starting states, rows chain_range(C_total, rank,
+    world), and C_total.  u_0 is one of
+      * the full ensemble (C_total, k) (n_total None or C_total): its rows
+        [lo, hi) are read (a memory-mapped .npy reads only those);
+      * a callable u_0(lo, hi) -> (hi - lo, k) (n_total required): the rank
+        builds only its own rows;
+      * this rank's own block (hi - lo, k) with n_total = C_total given: no
+        rank holds another's rows (per-rank memory stays
+        C_total / P whatever the node's ensemble)."""
+    if callable(u_0) and not isinstance(u_0, (np.ndarray, torch.Tensor)):
+        if n_total is None:
+            raise ValueError("a callable u_0(lo, hi) needs n_total (the node's chain count)")
+        lo, hi = chain_range(int(n_total), rank, world)
+        block = u_0(lo, hi)
+        if len(np.shape(block)) != 2 or np.shape(block)[0] != hi - lo:
+            raise ValueError(f"u_0({lo}, {hi}) must return ({hi - lo}, k) rows, got shape {np.shape(block)}")
+        return block, int(n_total)
+    if len(np.shape(u_0)) != 2:
+        raise ValueError("run_sharded needs u_0 of shape (chains, k)")
+    rows = int(np.shape(u_0)[0])
+    n_total = rows if n_total is None else int(n_total)
+    lo, hi = chain_range(n_total, rank, world)
+    if rows == n_total:  # the full ensemble: this rank's rows of it
+        return u_0[lo:hi], n_total
+    if rows != hi - lo:
+        raise ValueError(f"u_0 has {rows} rows: neither the {n_total} chains of the node nor rank {rank}'s "
+                         f"{hi - lo} (chain_range({n_total}, {rank}, {world}))")
+    return u_0, n_total
+
+
 def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200, keep="moments", group=None,
-                sample_file=None, gather="all", results="host"):
+                sample_file=None, gather="all", results="host", n_total=None):
     """MCMCSampler.run over the chains of every rank of a node, one process per GPU.
 
     make_sampler(chain_offset=...) builds this rank's sampler (the same
     proposer / accepter / potential / rng seed on every rank; the sampler's
-    chain_offset must be the one passed).  u_0 (C_total, k) is the full
-    ensemble's starting states on every rank (an array, e.g. a memory-mapped
-    .npy; each rank reads only its block of rows).  Rank r runs the
+    chain_offset must be the one passed).  u_0 gives the starting states:
+    the full ensemble (C_total, k) on every rank (an array, e.g. a
+    memory-mapped .npy; each rank reads only its block of rows), or -- with
+    n_total=C_total -- only this rank's block (hi - lo, k) or a callable
+    u_0(lo, hi) returning it (local_start), so that no rank allocates the
+    node's ensemble.  Rank r runs the
     chains chain_range(C_total, r, P) -- global ids, so every chain's
     trajectory is the one-process run's bit for bit -- and the per-chain
     results of all ranks are gathered by one all_gather_into_tensor (RCCL over
@@ -246,9 +280,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         raise ValueError("gather='mean' needs keep='moments'")
     if results == "device" and gather != "mean":
         raise ValueError("results='device' needs gather='mean' (the per-chain rows stay on their rank)")
-    if len(np.shape(u_0)) != 2:
-        raise ValueError("run_sharded needs u_0 of shape (chains, k)")
-    n_total = int(np.shape(u_0)[0])
+    local_u0, n_total = local_start(u_0, n_total, rank, world)
     lo, hi = chain_range(n_total, rank, world)
     sampler = make_sampler(chain_offset=lo)
     if sampler.chain_offset != lo:
@@ -256,7 +288,8 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     # gather="mean": the posterior mean's block sums run on the device sums the
     # sweeps left (MCMCSampler.last_device_sums) when the run was a device run
     sampler.keep_device_sums = gather == "mean"
-    local_u0 = u_0[lo:hi] if isinstance(u_0, torch.Tensor) else np.asarray(u_0[lo:hi], dtype=np.float64)
+    if not isinstance(local_u0, torch.Tensor):
+        local_u0 = np.asarray(local_u0, dtype=np.float64)
     sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
     t0 = time.perf_counter()
     res = sampler.run(local_u0, n_samples, burn_in=burn_in, sample_interval=sample_interval, keep=keep,
@@ -282,7 +315,10 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         rows = dsum[0] if dsum is not None else res["sum_u"].reshape(hi - lo, k)
         mean = ordered_sum_sharded(rows, group) / (float(n) * n_total)
         sampler.last_device_sums = None
-        return {"u": cols[0], "phi": phi_all, "accepts": acc_all, "sum_u": res["sum_u"],
+        # a device state is the checkpoint's own tensor (in the run's dtype):
+        # hand out an f64 copy, as the host path and MCMCSampler.run(keep='last') do
+        u_out = cols[0].to(torch.float64, copy=True) if isinstance(cols[0], torch.Tensor) else cols[0]
+        return {"u": u_out, "phi": phi_all, "accepts": acc_all, "sum_u": res["sum_u"],
                 "sum_u2": res["sum_u2"], "n": res["n"], "mean": mean, "rank": rank, "world": world,
                 "chain_range": (lo, hi), "local": res, "sampler": sampler, "run_seconds": run_s,
                 "gather_seconds": time.perf_counter() - t1}

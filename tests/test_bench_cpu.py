@@ -3,6 +3,8 @@ import json
 import subprocess
 import sys
 
+import pytest
+
 from conftest import REPO
 
 
@@ -46,6 +48,41 @@ def test_auto_steps_per_launch():
     assert bench.auto_per_launch(16384) == 1
     assert bench.auto_per_launch(8192) == 512  # strong scaling over 8 GPUs: long speculative launches
     assert bench.auto_per_launch(1) == 512
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 3, 4, 8])
+def test_default_line_is_the_metrics_ensemble_for_any_gpu_count(gpus):
+    """BASELINE's metric is 65 536 chains over the whole node: by default
+    `bench.py --gpus N` splits them over the N GPUs (strong scaling), and the
+    line's metric string names exactly the chains it timed."""
+    sys.path.insert(0, REPO)
+    import bench
+    from ip_mcmc_amd.shard import chain_range
+
+    metric = json.load(open(f"{REPO}/BASELINE.json"))["metric"]
+    scaling, total = bench.ensemble("cfg3", gpus)
+    assert scaling == "strong" and total == 65536
+    assert bench.metric_name("cfg3", "lorenz96_d40_rk4_2000_pcn", total) == metric
+    assert sum(b - a for a, b in (chain_range(total, r, gpus) for r in range(gpus))) == 65536
+    if gpus == 8:
+        assert chain_range(total, 7, 8) == (7 * 8192, 8 * 8192)  # 8 192 chains per GPU
+    # weak: 65 536 on every GPU -- a different ensemble, so a different metric string
+    scaling, total = bench.ensemble("cfg3", gpus, None, "weak")
+    assert total == 65536 * gpus
+    name = bench.metric_name("cfg3", "lorenz96_d40_rk4_2000_pcn", total)
+    assert (name == metric) == (gpus == 1)
+    assert f"{65536 * gpus:,} chains".replace(",", " ") in name
+    # configs 4 and 5: their node ensembles, split
+    assert bench.ensemble("cfg4", gpus) == ("strong", 16384)
+    assert bench.ensemble("cfg5", gpus) == ("strong", 1 << 20)
+
+
+def test_metric_names_the_chains_run():
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.metric_name("cfg3", "x", 8192) == "pCN steps/sec (whole node), Lorenz-96 d=40 T=2000, 8 192 chains"
+    assert bench.ensemble("cfg3", 1, 8192) == ("strong", 8192)
 
 
 def _committed_lines():

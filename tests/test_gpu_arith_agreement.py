@@ -91,3 +91,31 @@ def test_fma_and_reference_posteriors_agree_at_the_references_noise_level():
     assert r["max_z"] < Z_MAX, r
     assert abs(r["mean_z2"] - 1) < BAND, r
     assert abs(r["t2_over_d"] - 1) < BAND, r
+
+
+def test_fp32_and_fp64_posteriors_agree_at_the_references_noise_level():
+    """The precision twin of the test above: fp32 against fp64
+    (both FMA arith) at the headline shape and the reference's own r = 0.5
+    (lorenz_mcmc.py:92,111-112), 50 000 pCN steps per chain from independent
+    u_0 and seeds, the same stationarity and agreement bounds.  Config 5's
+    shape at r = 0.5 (10 min of GPU) stays a recorded tool run:
+    profiles/r5/posterior_prec_r05_long.jsonl."""
+    import torch
+
+    import posterior_agreement as PA
+
+    assert torch.cuda.is_available()
+    chains, n_seg, seg_len, beta, noise_r = RUN_R05
+    r = PA.measure("prec40", chains, n_seg, seg_len, beta, noise_r, paired=False)
+    print(r)
+    PA.record(r, "posterior_agreement.jsonl")
+    assert r["d"] == D and r["noise_r"] == 0.5 and r["pcn_steps"] == 50000 and r["rk4_steps"] == 2000
+    assert "burn_in_capped_from" not in r, r
+    for arm in ("fma_float64", "fma_float32"):
+        a = r[arm]
+        assert 0.02 < a["accept_rate"] < 0.98, a
+        assert a["half_z_max"] < Z_MAX and a["half_var_z_max"] < Z_MAX, a
+        assert a["rhat_max"] < 1.2, a
+    assert r["max_z"] < Z_MAX, r
+    assert abs(r["mean_z2"] - 1) < BAND, r
+    assert abs(r["t2_over_d"] - 1) < BAND, r

@@ -3,8 +3,8 @@ the final gather, rank-0 JSON line) rehearsed with 2 ranks on the one-GPU box:
 both ranks on cuda:0 and gloo for the collectives (RCCL needs one GPU per rank;
 the driver's 8-GPU runs use it).  Started both ways: under an external
 torch.distributed.run (the driver's form) and as plain `python bench.py --gpus 2`,
-which launches the ranks itself (weak scaling: the metric's 65 536 chains on every
-rank, the strong split beside it),
+which launches the ranks itself (strong scaling by default: the metric's 65 536
+chains split over the ranks, the weak figure -- 65 536 on every rank -- beside it),
 and the config-5 workload (2^20 chains over the ranks, f64, through
 shard.run_sharded with the rank-sequential posterior mean)."""
 import json
@@ -39,7 +39,7 @@ def test_bench_two_ranks_rehearsal():
     assert len(lines) == 1, r.stdout  # rank 0 prints one line
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["config"]["total_chains"] == 8192
+    assert line["config"]["total_chains"] == 8192 and "8 192 chains" in line["metric"]
     assert line["final_gather"]["rows"] == 8192 and "gloo" in line["final_gather"]["collective"]
     assert line["final_gather"]["mode"] == "mean"
     assert line["value"] > 0 and 0 < line["accept_rate"] < 1
@@ -53,12 +53,15 @@ def test_bench_gpus_2_launches_its_own_ranks():
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["config"]["total_chains"] == 131072 and line["config"]["chains_per_gpu"] == 65536
-    assert line["final_gather"]["rows"] == 131072 and line["final_gather"]["inside_timed_region"]
+    # BASELINE's metric is 65 536 chains over the whole node: split over the ranks
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["metric"] == json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+    assert line["config"]["total_chains"] == 65536 and line["config"]["chains_per_gpu"] == 32768
+    assert line["final_gather"]["rows"] == 65536 and line["final_gather"]["inside_timed_region"]
     ex = line["extra"]
-    assert ex["strong_scaling"]["total_chains"] == 65536 and ex["strong_scaling"]["chains_per_gpu"] == 32768
-    assert ex["strong_scaling"]["pcn_steps_per_s"] > 0
+    assert ex["weak_scaling"]["total_chains"] == 131072 and ex["weak_scaling"]["chains_per_gpu"] == 65536
+    assert ex["weak_scaling"]["pcn_steps_per_s"] > 0 and "131 072 chains" in ex["weak_scaling"]["metric"]
+    assert ex["run_e2e_moments"]["u0_rows_per_rank"] == 32768  # rank-local u_0
     assert ex["reference_arith_kernel_pcn_steps_per_s"] > 0 and ex["run_e2e_samples"]["pcn_steps_per_s"] > 0
     # value is the end-to-end run; the kernel leg is beside it
     assert line["value"] == ex["run_e2e_moments"]["pcn_steps_per_s"] and ex["kernel_pcn_steps_per_s"] > 0
@@ -66,11 +69,14 @@ def test_bench_gpus_2_launches_its_own_ranks():
     # value's data in HBM; the host-buffer run (PCIe included) beside it
     assert ex["run_e2e_moments"]["data_in_hbm"] and not ex["run_e2e_pcie"]["data_in_hbm"]
     assert ex["run_e2e_pcie"]["pcn_steps_per_s"] > 0
-    assert ex["mixing_posterior"]["total_chains"] == 131072 and ex["mixing_posterior"]["pcn_steps_per_s"] > 0
+    assert ex["mixing_posterior"]["total_chains"] == 65536 and ex["mixing_posterior"]["pcn_steps_per_s"] > 0
     # REFERENCE arith end to end beside value; the paired streams run at N = 1 only
     assert line["parity"]["reference_arith_value"] > 0 and "paired_identical_accept_frac" not in line["parity"]
     assert ex["configs"]["cfg4"]["f64"]["total_chains"] == 16384
     assert ex["configs"]["cfg5"]["f64"]["total_chains"] == 1 << 20 and ex["configs"]["cfg5"]["f32"]["pcn_steps_per_s"] > 0
+    ap = ex["configs"]["cfg5"]["arith_parity"]  # config 5's bit-exact carrier and its rate
+    assert ap["bit_exact_arith"] == "reference" and ap["bit_exact_pcn_steps_per_s"] > 0
+    assert 0 < ap["reference_frac_of_peak"] < ap["reference_op_ceiling_frac"] < 0.5
 
 
 def test_bench_cfg5_workload_two_ranks():

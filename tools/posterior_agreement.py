@@ -237,6 +237,9 @@ def measure(kind, chains, n_seg, seg_len, beta=0.2, r=R_NOISE, window=None, pair
     elif kind == "prec":
         d, n_rk = 256, 10000
         runs = (("fma", np.float64, 11, 5), ("fma", np.float32, 12, 6))
+    elif kind == "prec40":  # fp32 vs fp64 at the headline shape (the reference's noise level: tests/)
+        d, n_rk = 40, 2000
+        runs = (("fma", np.float64, 11, 5), ("fma", np.float32, 12, 6))
     else:
         raise ValueError(kind)
     t0 = time.perf_counter()

@@ -1,0 +1,58 @@
+#!/bin/bash
+# Round-6 GPU sessions: bash tools/sessions/r6.sh <name>
+# Every GPU step has its own time limit.  A step that faults, aborts or times
+# out ends the session (tests_ok lets pytest's "some tests failed" (rc 1)
+# through, so one red assertion does not hide the rest of the session).
+set -o pipefail
+cd "$(dirname "$0")/../.."
+O=gpurun_out/r6
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+export IPMC_RECORD_DIR=$O
+tests_ok() { "$@"; rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step failed rc=$rc: $*"; exit $rc; fi; }
+PYT="python -u -m pytest -v --timeout 600 --timeout-method thread"
+SQC="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+# the metric's 8-GPU share on one GPU: 8 192 chains (global ids 7*8192..), the driver's K = 20
+SHARD="python bench.py --chains 8192 --scaling strong --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity"
+case "$1" in
+  shard0)
+    # the 8 192-chain strong shard on the round-6 starting tree: the line twice,
+    # a kernel trace of the end-to-end leg, an SQ pass of the kernel leg
+    for i in 1 2; do
+      timeout -k 10 300 $SHARD >> $O/shard0_lines.jsonl 2>> $O/shard0.err || exit $?
+    done &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/shard0_trace -o run -- \
+      $SHARD > $O/shard0_trace.json 2> $O/shard0_trace.err &&
+    python tools/e2e_trace_summary.py $O/shard0_trace > $O/shard0_trace_summary.json &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQC --kernel-trace --output-format csv -d $O/shard0_sq -o run -- \
+      $SHARD --kernel-only > /dev/null 2>> $O/shard0.err &&
+    python tools/sq_summarize.py $O/shard0_sq 'sweep_kernel' > $O/shard0_sq.json
+    ;;
+  ab8)
+    # the 8 192-chain shard's kernel (d=40 on 8 lanes, one 20-step launch):
+    # product vs halo-first component order (hf), one-wave target (w1), RK
+    # loop unrolled by 2 (u2), interleaved twice; the headline kernel for hf
+    for i in 1 2; do
+      for v in product hf w1 u2; do
+        L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+        IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/shard_kernel_probe.py $v >> $O/ab8.jsonl || exit 1
+      done
+    done &&
+    for v in product hf; do
+      L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+      IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/arith_kernel_probe.py $v >> $O/ab8_headline.jsonl || exit 1
+    done
+    ;;
+  s1)
+    # strong scaling by default, rank-local u_0, fp32/fp64 at r = 0.5: the
+    # N-rank and shard tests, the new tolerance test; the host profile of the
+    # 8 192-chain end-to-end leg
+    tests_ok timeout -k 10 900 $PYT tests/test_gpu_bench_dist.py tests/test_gpu_shard.py \
+      "tests/test_gpu_arith_agreement.py::test_fp32_and_fp64_posteriors_agree_at_the_references_noise_level" \
+      > $O/pytest_s1.log 2>&1
+    timeout -k 10 200 python tools/probes/shard_e2e_profile.py 8192 20 3 s1 >> $O/shard_e2e.jsonl 2> $O/shard_e2e_prof_s1.txt
+    ;;
+  *)
+    echo "unknown session $1"; exit 2
+    ;;
+esac
