@@ -17,11 +17,13 @@ handing over host buffers (H2D of u_0, D2H of states and sums) is
 extra.run_e2e_pcie, the PCIe-inclusive rate.
 value = all chains of all ranks x K / that time.  The chains are independent
 units, sharded over the ranks with no collective on the data path (global
-chain ids, so every chain is the one-GPU run's bit for bit): cfg3 runs the
-metric's 65 536 chains on every GPU (weak scaling, the default), and at N > 1
-"extra.strong_scaling" carries the 65 536 chains split over the N GPUs.
-Configs 4 and 5 state their ensembles per node, so --workload cfg4 / cfg5
-split them (strong).
+chain ids, so every chain is the one-GPU run's bit for bit).  BASELINE's
+metric is 65 536 chains over the whole node, so cfg3 splits them over the N
+GPUs (strong scaling, the default: 8 192 chains per GPU at N = 8), and at
+N > 1 "extra.weak_scaling" carries 65 536 chains on every GPU under its own
+metric string.  Configs 4 and 5 state their ensembles per node too, so
+--workload cfg4 / cfg5 split them the same way.  Every rank holds only its
+own block of u_0 (run_sharded(n_total=...)).
 
 extra.kernel_*: the same sweep kernel on device-resident state (raw
 ipmc_pcn_sweep launches, one pCN step per launch for a full GPU, HIP events

@@ -62,6 +62,13 @@ extern "C" {
 
 #define IPMC_ABI_VERSION 13
 
+/* entry points kept for older callers but no longer on the product path */
+#if defined(__GNUC__) || defined(__clang__)
+#define IPMC_DEPRECATED(msg) __attribute__((deprecated(msg)))
+#else
+#define IPMC_DEPRECATED(msg)
+#endif
+
 typedef enum {
   IPMC_OK = 0,
   IPMC_ERR_INVALID = 1,     /* bad argument (shape, null pointer, range) */
@@ -249,10 +256,13 @@ int ipmc_burn_in(const void* x, int32_t dtype, int64_t n_chains, int32_t n_vars,
                  int64_t stride_var, int64_t stride_t, int32_t window, double threshold, uint32_t* flags_scratch,
                  int64_t* out, void* stream);
 
-/* (ABI 12) acc[j] = (((acc[j] + rows[0][j]/div) + rows[1][j]/div) + ...) for j < k over the n_rows rows
-   (row r at rows + r*row_stride doubles), strictly in row order -- one dependent chain of adds per column
-   (the posterior mean uses ipmc_block_sums since ABI 13), equal bit for bit to ipmc_host_ordered_sum (ipmc_host.h);
-   div == 1 adds the rows as they are.  Device pointers; acc [k] in/out. */
+/* DEPRECATED since ABI 13 -- not on the product path: the posterior mean is ipmc_block_sums (below) + the
+   block sums in block order, which no rank has to wait for.  Kept (exported, tested) for callers of ABI 12.
+   (ABI 12) acc[j] = (((acc[j] + rows[0][j]/div) + rows[1][j]/div) + ...) for j < k over the n_rows rows
+   (row r at rows + r*row_stride doubles), strictly in row order -- one dependent chain of adds per column,
+   equal bit for bit to ipmc_host_ordered_sum (ipmc_host.h); div == 1 adds the rows as they are.
+   Device pointers; acc [k] in/out. */
+IPMC_DEPRECATED("ipmc_block_sums (ABI 13) forms the posterior mean")
 int ipmc_ordered_sum(const double* rows, int64_t n_rows, int64_t k, int64_t row_stride, double div, double* acc,
                      void* stream);
 

@@ -87,6 +87,12 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
 #else
 #define IPMC_L96_RK_UNROLL
 #endif
+#ifndef IPMC_L96_PREWAIT  // experiments: 0 = the loads of x(0) waited for inside the RK loop
+#define IPMC_L96_PREWAIT 0
+#endif
+#ifndef IPMC_L96_PAIR_MAX_M  // two RK4 steps per loop iteration up to this many components per lane
+#define IPMC_L96_PAIR_MAX_M 0
+#endif
 
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
 // V is the per-lane storage type (float, double, or f32x2 = two fp32 chains),
@@ -105,14 +111,34 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     x[j] = P::of(x0[j]);
     ob[j] = P::of((S)0);
   }
-  IPMC_L96_RK_UNROLL
-  for (int n = 0; n < nsteps; ++n) {
+#if IPMC_L96_PREWAIT
+  // x(0) is first read inside the RK loop, so the memory-wait pass put its
+  // s_waitcnt at the loop top, where it issues every RK4 step (2 of the 129
+  // instructions per step at 8 lanes per chain, whose one wave per SIMD
+  // issues every instruction in its own 4-cycle slot).  An opaque use here
+  // makes the loads complete before the loop.
+#pragma unroll
+  for (int j = 0; j < M; ++j) asm volatile("" : "+v"(x[j]));
+#endif
+  auto rk4 = [&]() {
     V acc[M], xs[M];
     l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);
     l96_stage<V, M, LPC, FM, 2, IL>(xs, xs, x, acc, ob, F, h2, two, lane);
     l96_stage<V, M, LPC, FM, 3, IL>(xs, xs, x, acc, ob, F, h, two, lane);
     l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
+  };
+  int n = 0;
+  if constexpr (M <= IPMC_L96_PAIR_MAX_M) {
+    // two RK4 steps per iteration: the loop's 3 scalar instructions (counter,
+    // compare, branch) per two steps instead of one, where a lane's step is
+    // short (M <= 8: 127 instructions at M = 5, the wave alone on its SIMD)
+    for (; n + 1 < nsteps; n += 2) {
+      rk4();
+      rk4();
+    }
   }
+  IPMC_L96_RK_UNROLL
+  for (; n < nsteps; ++n) rk4();
   const V nn = P::of((S)nsteps);
 #pragma unroll
   for (int j = 0; j < M; ++j) g[j] = ob[j] / nn;

@@ -58,6 +58,30 @@ def to_device(x, dtype, device):
     return torch.as_tensor(np.asarray(x, dtype=np.float64), dtype=dtype).to(device).contiguous()
 
 
+# small read-only problem constants (y, 1/γ, sqrt diag C, ...) by content: a
+# run() re-uses the device copy of the same values instead of a synchronous
+# host-to-device copy each (three of them were ~0.1 ms of an 8 192-chain
+# run's set-up, during which the GPU waits)
+_CONST_MAX_BYTES = 1 << 16
+_CONST_CACHE = {}
+
+
+def const_to_device(x, dtype, device):
+    """to_device for a small array the kernels only read: the device copy is
+    shared by every call with the same values, dtype and device.  Callers
+    must not write to the result.  Arrays above 64 KiB are copied as usual."""
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if a.nbytes > _CONST_MAX_BYTES:
+        return to_device(a, dtype, device)
+    key = (a.shape, a.tobytes(), str(dtype), str(device))
+    t = _CONST_CACHE.get(key)
+    if t is None:
+        if len(_CONST_CACHE) >= 256:
+            _CONST_CACHE.clear()
+        t = _CONST_CACHE[key] = to_device(a, dtype, device)
+    return t
+
+
 def rect_copy_available():
     """The block-wise sample copy goes through libipmc (ipmc_copy_rows_d2h),
     which runs on the HIP runtime the caller's streams belong to: always
@@ -75,7 +99,9 @@ def copy_rows_d2h(dst, dst_pitch, src, src_pitch, width, rows, stream):
 
 
 def ordered_sum(rows, acc, div=1.0):
-    """acc (device f64 [k], in place) + rows[0]/div + rows[1]/div + ... strictly
+    """DEPRECATED (ABI 13; not on the product path: the posterior mean is
+    block_sums + the block sums in order, shard.ordered_sum_sharded).
+    acc (device f64 [k], in place) + rows[0]/div + rows[1]/div + ... strictly
     in row order on the device (ipmc_ordered_sum, the current stream): the bits
     of the host library's ipmc_host_ordered_sum.  rows: device f64 [n, k] with
     unit column stride."""

@@ -238,18 +238,18 @@ class MCMCSampler:
         phi = torch.empty((n_chains,), dtype=td, device=device)
         accepts = torch.zeros((n_chains,), dtype=torch.int64, device=device)
         calls = torch.zeros((n_chains,), dtype=torch.int64, device=device) if plan.counted_inner else None
-        y_t = dev.to_device(plan.y_eff, td, device)
-        gi_t = dev.to_device(plan.gamma_inv, td, device)
-        sq_t = None if plan.prior_sqrt is None else dev.to_device(plan.prior_sqrt, td, device)
-        chol_t = None if plan.prior_chol is None else dev.to_device(plan.prior_chol, td, device)
+        y_t = dev.const_to_device(plan.y_eff, td, device)
+        gi_t = dev.const_to_device(plan.gamma_inv, td, device)
+        sq_t = None if plan.prior_sqrt is None else dev.const_to_device(plan.prior_sqrt, td, device)
+        chol_t = None if plan.prior_chol is None else dev.const_to_device(plan.prior_chol, td, device)
         keep_alive = [y_t, gi_t, sq_t, chol_t]
         box_ptrs = (None, None, None)
         if plan.box is not None:
             arrs = plan.box.arrays(k)
-            ts = [None if a is None else dev.to_device(a, td, device) for a in arrs]
+            ts = [None if a is None else dev.const_to_device(a, td, device) for a in arrs]
             keep_alive += [t for t in ts if t is not None]
             box_ptrs = tuple(dev.ptr(t) for t in ts)
-        reg_t = None if plan.reg_scale is None else dev.to_device(plan.reg_scale, td, device)
+        reg_t = None if plan.reg_scale is None else dev.const_to_device(plan.reg_scale, td, device)
         keep_alive.append(reg_t)
         model, _ = plan.G.model(td, device)
 

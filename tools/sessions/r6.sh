@@ -52,6 +52,36 @@ case "$1" in
       > $O/pytest_s1.log 2>&1
     timeout -k 10 200 python tools/probes/shard_e2e_profile.py 8192 20 3 s1 >> $O/shard_e2e.jsonl 2> $O/shard_e2e_prof_s1.txt
     ;;
+  ab9)
+    # x(0)'s loads waited for before the RK loop (pw: 129 -> 127 instructions
+    # per RK4 step at 8 lanes) and two RK4 steps per iteration (pwp: 126.5),
+    # against the product, interleaved three times; the headline kernel; the
+    # 8 192-chain end-to-end leg with the cached constants, product vs pwp
+    for i in 1 2 3; do
+      for v in product pw pwp; do
+        L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+        IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/shard_kernel_probe.py $v >> $O/ab9.jsonl || exit 1
+      done
+    done &&
+    for v in product pw; do
+      L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+      IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/arith_kernel_probe.py $v >> $O/ab9_headline.jsonl || exit 1
+    done &&
+    for i in 1 2; do
+      for v in product pwp; do
+        L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+        IPMC_LIB_PATH=$L timeout -k 10 200 python tools/probes/shard_e2e_profile.py 8192 20 3 $v >> $O/ab9_e2e.jsonl \
+          2> /dev/null || exit 1
+      done
+    done
+    ;;
+  gloo8)
+    # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
+    # GPU (strong scaling by default: 65 536 chains over the node under
+    # BASELINE's metric, 8 192 per rank; the weak figure in extra)
+    timeout -k 10 900 python bench.py --gpus 8 --steps 20 --warmup 5 --dist-backend gloo --share-device --no-cpu \
+      --no-configs > $O/bench_gloo8.json 2> $O/bench_gloo8.err
+    ;;
   *)
     echo "unknown session $1"; exit 2
     ;;
