@@ -301,12 +301,14 @@ def log(msg):
 
 
 def barrier(world):
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
 
 
 def max_over_ranks(x, world, dev):
-    if world > 1:
+    """The max of x over the ranks of the process group (RCCL on the device
+    with backend "nccl"); x itself without one."""
+    if dist.is_initialized():
         t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         x = float(t.item())

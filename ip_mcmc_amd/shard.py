@@ -127,7 +127,8 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
         a = local.detach().cpu().numpy() if isinstance(local, torch.Tensor) else local
         rows = np.asarray(a, dtype=np.float64).reshape(len(a), k)
     n_local = int(rows.shape[0])
-    if world > 1:
+    comm = _dist_on()
+    if comm:  # (a one-rank process group too: the collectives run, over RCCL on the GPU)
         dev = _comm_device(group)
         counts = torch.empty(world, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(counts, torch.tensor([n_local], dtype=torch.int64, device=dev), group=group)
@@ -155,7 +156,7 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
         h, (c0, c1), t = _split(int(los[r]), int(los[r + 1]), block)
         return ((c1 - c0) + sum(seg[1] - seg[0] for seg in (h, t) if seg is not None)) * k
 
-    if world > 1:
+    if comm:
         per = max(max(size(r) for r in range(world)), 1)
         buf = torch.zeros(per, dtype=torch.float64, device=dev)
         buf[: mine.size] = torch.from_numpy(mine).to(dev)
@@ -180,6 +181,12 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
     for b, pc in pieces.items():  # a block over several ranks: its rows in rank order, from zero
         sums[b] = _seq_sum(np.concatenate(pc), np.zeros(k), div)
     return _seq_sum(sums, np.zeros(k)).reshape(shape)
+
+
+def _dist_on():
+    """A process group is initialised: the gathers run as collectives (RCCL
+    with backend "nccl") even for a one-rank group."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def world_info(group=None):
@@ -303,7 +310,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
             np.asarray(st.accepts, dtype=np.float64).reshape(hi - lo, 1)]  # counts < 2^53: exact
     if gather == "mean":
         t1 = time.perf_counter()
-        if world > 1:
+        if _dist_on():
             small = np.concatenate(cols[1:], axis=1)
             small = gather_chains(torch.from_numpy(np.ascontiguousarray(small)).to(_comm_device(group)), n_total,
                                   group).cpu().numpy()
@@ -325,7 +332,7 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     t1 = time.perf_counter()
     out = {"rank": rank, "world": world, "chain_range": (lo, hi), "local": res, "sampler": sampler,
            "run_seconds": run_s}
-    if world == 1:  # nothing to gather: this process's arrays are the result
+    if not _dist_on():  # no process group, one rank: this process's arrays are the result
         out.update(u=cols[0], phi=cols[1][:, 0], accepts=np.asarray(st.accepts, dtype=np.int64))
         if keep == "moments":
             out.update(sum_u=res["sum_u"].reshape(hi - lo, k), sum_u2=res["sum_u2"].reshape(hi - lo, k), n=res["n"])

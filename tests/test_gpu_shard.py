@@ -236,3 +236,50 @@ def test_results_on_the_device_equal_the_host_results():
         assert np.array_equal(dd[key], one[key]), key
     assert np.array_equal(dd["u"].cpu().numpy(), one["u"]) and np.array_equal(dd["sum_u"].cpu().numpy(),
                                                                                one["sum_u"])
+    # the returned state is a copy, not the checkpoint's own tensor
+    ck = dd["sampler"].checkpoint().u_device
+    before = ck.clone()
+    dd["u"].add_(1.0)
+    assert torch.equal(ck, before) and dd["u"].dtype == torch.float64
+
+
+def _rccl_worker(rank, world, port, out_path):
+    sys.path.insert(0, REPO)
+    import bench
+    from ip_mcmc_amd.shard import run_sharded
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    # every collective of the product path, over RCCL on the device
+    ga = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="all")
+    gm = run_sharded(_make_sampler, torch.as_tensor(_u0(), device=dev), n_samples=1, burn_in=0, sample_interval=6,
+                     keep="moments", gather="mean", results="device")
+    mx = bench.max_over_ranks(2.5, world, dev)
+    dist.barrier()
+    np.savez(out_path, u=ga["u"], phi=ga["phi"], acc=ga["accepts"], sum_u=ga["sum_u"], mean_all=ga["mean"],
+             mean=gm["mean"], phi_m=gm["phi"], acc_m=gm["accepts"], mx=mx)
+    dist.destroy_process_group()
+
+
+def test_rccl_collectives_of_the_product_path(tmp_path):
+    """The RCCL branches on hardware: a one-rank "nccl" process group (RCCL
+    refuses two ranks on one GPU, profiles/r5/rccl_probe.json) runs every
+    collective run_sharded and bench.py issue -- the packed all_gather
+    (gather='all'), the counts / block-sum all_gathers (gather='mean', device
+    rows), the MAX all_reduce of the wall time -- on device tensors.  The
+    results equal the process-group-free run bit for bit."""
+    from ip_mcmc_amd.shard import run_sharded
+
+    out = str(tmp_path / "rccl_world1.npz")
+    mp.start_processes(_rccl_worker, args=(1, _free_port(), out), nprocs=1, start_method="spawn")
+    got = np.load(out)
+    one = run_sharded(_make_sampler, _u0(), n_samples=1, burn_in=0, sample_interval=6, keep="moments", gather="all")
+    for key, want in (("u", one["u"]), ("phi", one["phi"]), ("acc", one["accepts"]), ("sum_u", one["sum_u"]),
+                      ("mean_all", one["mean"]), ("mean", one["mean"]), ("phi_m", one["phi"]),
+                      ("acc_m", one["accepts"])):
+        assert np.array_equal(got[key], want), key
+    assert float(got["mx"]) == 2.5

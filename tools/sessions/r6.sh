@@ -82,6 +82,12 @@ case "$1" in
     timeout -k 10 900 python bench.py --gpus 8 --steps 20 --warmup 5 --dist-backend gloo --share-device --no-cpu \
       --no-configs > $O/bench_gloo8.json 2> $O/bench_gloo8.err
     ;;
+  s2)
+    # ab9, then the shard tests with the one-rank RCCL group, the gloo 8-rank line
+    bash tools/sessions/r6.sh ab9 &&
+    { tests_ok timeout -k 10 600 $PYT tests/test_gpu_shard.py > $O/pytest_s2.log 2>&1; } &&
+    bash tools/sessions/r6.sh gloo8
+    ;;
   *)
     echo "unknown session $1"; exit 2
     ;;
