@@ -90,8 +90,11 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
 #ifndef IPMC_L96_PREWAIT  // experiments: 0 = the loads of x(0) waited for inside the RK loop
 #define IPMC_L96_PREWAIT 0
 #endif
-#ifndef IPMC_L96_PAIR_MAX_M  // two RK4 steps per loop iteration up to this many components per lane
+#ifndef IPMC_L96_PAIR_MAX_M  // IPMC_L96_RK_PER_ITER RK4 steps per loop iteration up to this many components per lane
 #define IPMC_L96_PAIR_MAX_M 0
+#endif
+#ifndef IPMC_L96_RK_PER_ITER
+#define IPMC_L96_RK_PER_ITER 2
 #endif
 
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
@@ -128,13 +131,18 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
   };
   int n = 0;
-  if constexpr (M <= IPMC_L96_PAIR_MAX_M) {
-    // two RK4 steps per iteration: the loop's 3 scalar instructions (counter,
-    // compare, branch) per two steps instead of one, where a lane's step is
-    // short (M <= 8: 127 instructions at M = 5, the wave alone on its SIMD)
-    for (; n + 1 < nsteps; n += 2) {
-      rk4();
-      rk4();
+  // R RK4 steps per loop iteration where a lane's step is short: the loop's
+  // scalar counter / compare / branch then issue once per R steps.  A wave
+  // alone on its SIMD (8 192 chains of d=40 on 8 lanes: M = 5, 127
+  // instructions per step) issues every instruction in its own 4-cycle slot,
+  // scalar ones included (profiles/r6/shard_kernel_ab9.jsonl: R = 2 is 2.2 %
+  // faster there; the loads' s_waitcnt at the loop top, satisfied after the
+  // first step, cost nothing)
+  constexpr int R = (M <= IPMC_L96_PAIR_MAX_M) ? IPMC_L96_RK_PER_ITER : 1;
+  if constexpr (R > 1) {
+    for (; n + R <= nsteps; n += R) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) rk4();
     }
   }
   IPMC_L96_RK_UNROLL

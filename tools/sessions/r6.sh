@@ -75,6 +75,24 @@ case "$1" in
       done
     done
     ;;
+  ab10)
+    # R RK4 steps per loop iteration: R = 2 up to M = 10 (r2m10), R = 4 up to
+    # M = 10 (r4m10), R = 2 up to M = 20 (r2m20, the headline kernel too), at
+    # the per-GPU shares of N = 8 / 4 / 2 (8 192 / 16 384 / 32 768 chains, one
+    # wave per SIMD each) and the headline, interleaved twice
+    for i in 1 2; do
+      for c in 8192 16384 32768; do
+        for v in product r2m10 r4m10 r2m20; do
+          L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+          IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/shard_kernel_probe.py $v 20 $c 2 >> $O/ab10.jsonl || exit 1
+        done
+      done
+      for v in product r2m20; do
+        L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+        IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/arith_kernel_probe.py $v >> $O/ab10_headline.jsonl || exit 1
+      done
+    done
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
@@ -87,6 +105,41 @@ case "$1" in
     bash tools/sessions/r6.sh ab9 &&
     { tests_ok timeout -k 10 600 $PYT tests/test_gpu_shard.py > $O/pytest_s2.log 2>&1; } &&
     bash tools/sessions/r6.sh gloo8
+    ;;
+  final)
+    # the final tree: the whole suite and smoke, then the published line with
+    # its same-box profiles -- three PMC passes of the kernel leg (bench
+    # --kernel-only), the line reading them (default K/W and the driver's
+    # K=20 W=5), a kernel trace + stats of the kernel leg restricted to the
+    # timed launches, the f32 PMC passes
+    B="python bench.py --kernel-only --no-cpu --steps 5 --warmup 1"
+    SQ5="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_final.log 2>&1
+    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_final.txt 2>&1 &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc64/fetch -o run -- $B > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc64/write -o run -- $B > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQ5 --kernel-trace --output-format csv -d $O/pmc64/sq -o run -- $B > /dev/null &&
+    python tools/pmc_summarize.py $O/pmc64 f64 65536 $O/pmc_l96_f64.json 6 &&
+    timeout -k 10 600 python bench.py --pmc-file $O/pmc_l96_f64.json > $O/bench_line.json 2> $O/bench_line.err &&
+    timeout -k 10 600 python bench.py --steps 20 --warmup 5 --pmc-file $O/pmc_l96_f64.json > $O/bench_line_k20.json \
+        2> $O/bench_line_k20.err &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
+        python bench.py --kernel-only --no-cpu > $O/bench_kernel_only.json 2> $O/bench_kernel_only.err &&
+    python tools/trace_summary.py $O/trace 200 10 $O/bench_line.json > $O/bench_kernel_trace_summary.json &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc32/fetch -o run -- $B --dtype f32 > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc32/write -o run -- $B --dtype f32 > /dev/null &&
+    timeout -s KILL 120 rocprofv3 --pmc $SQ5 --kernel-trace --output-format csv -d $O/pmc32/sq -o run -- $B --dtype f32 > /dev/null &&
+    python tools/pmc_summarize.py $O/pmc32 f32 65536 $O/pmc_l96_f32.json 6
+    ;;
+  shards)
+    # the per-GPU shares of the metric's 65 536 chains at N = 2, 4, 8 (strong
+    # scaling), each on this one GPU at the driver's K = 20, twice
+    for i in 1 2; do
+      for c in 32768 16384 8192; do
+        timeout -k 10 300 python bench.py --chains $c --steps 20 --warmup 5 --no-cpu --no-extra --no-configs \
+          --no-parity >> $O/shards_k20.jsonl 2>> $O/shards.err || exit 1
+      done
+    done
     ;;
   *)
     echo "unknown session $1"; exit 2
