@@ -90,11 +90,13 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
 #ifndef IPMC_L96_PREWAIT  // experiments: 0 = the loads of x(0) waited for inside the RK loop
 #define IPMC_L96_PREWAIT 0
 #endif
-#ifndef IPMC_L96_PAIR_MAX_M  // IPMC_L96_RK_PER_ITER RK4 steps per loop iteration up to this many components per lane
-#define IPMC_L96_PAIR_MAX_M 0
+// IPMC_L96_RK_PER_ITER RK4 steps per loop iteration up to IPMC_L96_PAIR_MAX_M
+// components per lane (l96_forward; profiles/r6/shard_kernel_ab10.jsonl)
+#ifndef IPMC_L96_PAIR_MAX_M
+#define IPMC_L96_PAIR_MAX_M 10
 #endif
 #ifndef IPMC_L96_RK_PER_ITER
-#define IPMC_L96_RK_PER_ITER 2
+#define IPMC_L96_RK_PER_ITER 4
 #endif
 
 // Time-averaged RK4 trajectory: g[j] = (Σ_{n=1..N} x_n[j]) / N.
@@ -131,13 +133,16 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
   };
   int n = 0;
-  // R RK4 steps per loop iteration where a lane's step is short: the loop's
-  // scalar counter / compare / branch then issue once per R steps.  A wave
-  // alone on its SIMD (8 192 chains of d=40 on 8 lanes: M = 5, 127
+  // R RK4 steps per loop iteration where a lane's step is short (M <= 10):
+  // the loop's scalar counter / compare / branch then issue once per R steps.
+  // A wave alone on its SIMD (8 192 chains of d=40 on 8 lanes: M = 5, 127
   // instructions per step) issues every instruction in its own 4-cycle slot,
-  // scalar ones included (profiles/r6/shard_kernel_ab9.jsonl: R = 2 is 2.2 %
-  // faster there; the loads' s_waitcnt at the loop top, satisfied after the
-  // first step, cost nothing)
+  // scalar ones included: R = 2 / 4 run the 8 192-chain sweep 1.5-2.2 / 2.4-
+  // 3.5 % faster, 16 384 chains (M = 10) ~1 %; at M = 20 R = 2 gains ~1 % at
+  // one wave per SIMD but not at the headline's two, so M = 20 keeps R = 1
+  // (profiles/r6/shard_kernel_ab9.jsonl, shard_kernel_ab10.jsonl).  The
+  // loads' s_waitcnt at the loop top, satisfied after the first step, cost
+  // nothing (IPMC_L96_PREWAIT A/B, same files).
   constexpr int R = (M <= IPMC_L96_PAIR_MAX_M) ? IPMC_L96_RK_PER_ITER : 1;
   if constexpr (R > 1) {
     for (; n + R <= nsteps; n += R) {

@@ -93,6 +93,25 @@ case "$1" in
       done
     done
     ;;
+  ab11)
+    # what keep="moments"' per-step sums cost the 8 192 / 65 536-chain sweeps (sums vs none, interleaved)
+    for i in 1 2 3; do
+      for c in 8192 65536; do
+        timeout -k 10 120 python tools/probes/shard_kernel_probe.py nosums 20 $c 2 >> $O/ab11.jsonl &&
+        timeout -k 10 120 python tools/probes/shard_kernel_probe.py sums 20 $c 2 sums >> $O/ab11.jsonl || exit 1
+      done
+    done
+    ;;
+  s3)
+    bash tools/sessions/r6.sh ab10 && bash tools/sessions/r6.sh ab11
+    ;;
+  s4)
+    # the tree with R = 4 RK4 steps per iteration up to M = 10: the whole suite,
+    # smoke, the per-GPU shares at K = 20
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_s4.log 2>&1
+    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s4.txt 2>&1 &&
+    bash tools/sessions/r6.sh shards
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
