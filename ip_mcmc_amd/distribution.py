@@ -65,8 +65,11 @@ class GaussianDistribution(DistributionBase):
     # ---------------------------------------------------------------- shape
     @property
     def is_diagonal(self):
-        c = self.covariance
-        return bool(np.all(c == np.diag(np.diag(c))))
+        # decided once, like the factor L above (every run() asks, three times)
+        if getattr(self, "_diag_of", None) is not self.covariance:
+            c = self.covariance
+            self._is_diag, self._diag_of = bool(np.all(c == np.diag(np.diag(c)))), c
+        return self._is_diag
 
     @property
     def covariance_diagonal(self):

@@ -112,6 +112,11 @@ case "$1" in
     timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_s4.txt 2>&1 &&
     bash tools/sessions/r6.sh shards
     ;;
+  prof)
+    # host-side profile (microseconds per function) of the 8 192-chain end-to-end leg
+    timeout -k 10 200 python tools/probes/shard_e2e_profile.py 8192 20 4 prof >> $O/shard_e2e_prof.jsonl \
+      2> $O/shard_e2e_prof_us.txt
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
