@@ -62,6 +62,14 @@ class GaussianDistribution(DistributionBase):
         self.L = np.linalg.cholesky(covariance)
         self._logdet = 2.0 * float(np.sum(np.log(np.diag(self.L))))
 
+    def centred(self):
+        """N(0, C) sharing this distribution's covariance and its factor L (no
+        second factorization)."""
+        w = object.__new__(type(self))
+        w.__dict__.update(self.__dict__)
+        w.mean = np.zeros_like(self.mean)
+        return w
+
     # ---------------------------------------------------------------- shape
     @property
     def is_diagonal(self):

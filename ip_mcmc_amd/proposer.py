@@ -13,6 +13,15 @@ import numpy as np
 from .distribution import GaussianDistribution
 
 
+
+def _centred(prior):
+    """N(0, C) of the prior N(m, C), as proposer.py builds its noise
+    distribution: the prior's Cholesky factor is reused (a new factorization
+    per sampler was ~0.2 ms of every run_sharded call before any GPU work)."""
+    if isinstance(prior, GaussianDistribution):
+        return prior.centred()
+    return GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+
 class ProposerBase(ABC):
     """proposer.py:8-11."""
 
@@ -28,7 +37,7 @@ class ConstStepStandardRWProposer(ProposerBase):
 
     def __init__(self, delta, prior):
         self.prefactor = np.sqrt(2 * delta)
-        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+        self.w = _centred(prior)
 
     def device_step(self):
         return float(self.prefactor), 1.0
@@ -51,7 +60,7 @@ class VarStepStandardRWProposer(ProposerBase):
         self.prefactor = np.sqrt(2)
         self.delta = delta
         self.i = 0
-        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+        self.w = _centred(prior)
 
     def beta_schedule(self, i0, n):
         sched = np.empty((n, 2), dtype=np.float64)
@@ -94,7 +103,7 @@ class ConstSteppCNProposer(ProposerBase):
         assert 0 <= beta <= 1, "beta has to be in [0,1]"
         self.beta = beta
         self.contraction = np.sqrt(1 - beta**2)  # proposer.py:77
-        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+        self.w = _centred(prior)
 
     def device_step(self):
         return float(self.beta), float(self.contraction)
@@ -117,7 +126,7 @@ class VarSteppCNProposer(ProposerBase):
     def __init__(self, beta, prior):
         self.beta = beta
         self.i = 0
-        self.w = GaussianDistribution(mean=np.zeros_like(prior.mean), covariance=prior.covariance)
+        self.w = _centred(prior)
 
     def beta_schedule(self, i0, n):
         b = np.array([float(self.beta(i0 + j + 1)) for j in range(n)], dtype=np.float64)

@@ -234,7 +234,8 @@ class MCMCSampler:
         if isinstance(self.accepter, CountedAccepter):
             self.accepter.reset()  # sampler.py:15-16
 
-        stream = dev.stream_handle(device)
+        cur_stream = torch.cuda.current_stream(device)  # looked up once (~13 us a call)
+        stream = cur_stream.cuda_stream
         phi = torch.empty((n_chains,), dtype=td, device=device)
         accepts = torch.zeros((n_chains,), dtype=torch.int64, device=device)
         calls = torch.zeros((n_chains,), dtype=torch.int64, device=device) if plan.counted_inner else None
@@ -280,7 +281,7 @@ class MCMCSampler:
         if resume and u_0.phi.shape[0] != n_chains:
             raise ValueError("ChainState phi does not match its u")
         ev_setup = torch.cuda.Event(enable_timing=True)  # the GPU work of the set-up: Φ(u0)
-        ev_setup.record(torch.cuda.current_stream(device))
+        ev_setup.record(cur_stream)
         if resume and u_0.dtype == state_dtype and u_0.accept_kind != "generic":
             phi.copy_(dev.to_device(u_0.phi, td, device))
         else:
@@ -353,7 +354,7 @@ class MCMCSampler:
 
         t0 = time.perf_counter()
         ev_first = torch.cuda.Event(enable_timing=True)
-        ev_first.record(torch.cuda.current_stream(device))
+        ev_first.record(cur_stream)
         spl = _steps_per_launch(model, n_chains)
         n_burn = max(0, burn_in - sample_interval)  # sampler.py:18
         for c0 in range(0, n_burn, spl):
@@ -410,7 +411,7 @@ class MCMCSampler:
                 samples = writer.flush(i - slot, slot + nb)
             if overlap:
                 ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(device))
+                ev.record(cur_stream)
                 copies.append((i, i + nb, ev))
             i += nb
         for i in range(0 if not blockwise else n_samples, n_samples):  # sampler.py:23-28
@@ -431,7 +432,7 @@ class MCMCSampler:
         if sink is not None:
             writer.finish()
         ev_swept = torch.cuda.Event(enable_timing=True)
-        ev_swept.record(torch.cuda.current_stream(device))
+        ev_swept.record(cur_stream)
         # the host copy of the samples goes to page-locked memory (~57 GB/s
         # instead of ~5 GB/s pageable on the MI355X box, profiles/r1/d2h_probe.txt);
         # allocating it here overlaps the allocation with the queued sweeps
