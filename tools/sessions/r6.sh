@@ -117,6 +117,10 @@ case "$1" in
     timeout -k 10 200 python tools/probes/shard_e2e_profile.py 8192 20 4 prof >> $O/shard_e2e_prof.jsonl \
       2> $O/shard_e2e_prof_us.txt
     ;;
+  s5)
+    # the host trims: the 8 192-chain profile again, then the final session
+    bash tools/sessions/r6.sh prof && bash tools/sessions/r6.sh shards && bash tools/sessions/r6.sh final
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
