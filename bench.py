@@ -603,7 +603,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", 0 if args.share_device else local)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # a process group for N > 1, and for one rank under a launcher
+    # (torch.distributed.run sets MASTER_ADDR): then every collective of the
+    # line -- barriers, the gathers, the max over ranks -- runs over RCCL even
+    # on a one-GPU box (tests/test_gpu_bench_dist.py)
+    grouped = world > 1 or (env_world is not None and "MASTER_ADDR" in os.environ)
+    if grouped:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -665,7 +670,7 @@ def main():
                       "(block sums of 1 024 chains on each rank's GPU, shared blocks and block sums in one all_gather)",
               "collective": (f"all_gather_into_tensor ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
                              + (" + block-sum all_gather" if gather_mode == "mean" else "")
-                             if world > 1 else "none (one rank)"),
+                             if grouped else "none (one rank)"),
               "rows": int(res["phi"].shape[0]), "inside_timed_region": not args.kernel_only}
     assert np.isfinite(res["phi"]).all() and np.isfinite(res["mean"]).all()
     accept_rate = e2e["accept_rate"]
@@ -845,7 +850,7 @@ def main():
             "extra": extra,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

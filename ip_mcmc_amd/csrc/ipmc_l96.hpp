@@ -25,44 +25,27 @@ namespace ipmc {
 // bits do not change.  The stage input's halos are fetched before anything is
 // written, and the old X_{j-1}, X_{j-2} ride along in p1, p2, so `in` may alias
 // `xs`: one array of M values fewer live in the RK loop.
-// Component order inside a stage (experiments: -DIPMC_L96_HALO_FIRST=1): the
-// components whose new values the neighbour lanes read next stage (0, M-1,
-// M-2) first, the interior after them, so the next stage's DPP halo moves can
-// issue while the interior still computes.  The per-component operations are
-// the same in either order, so the bits are too.
-#ifndef IPMC_L96_HALO_FIRST
-#define IPMC_L96_HALO_FIRST 0
-#endif
-template <int M>
-__device__ __forceinline__ constexpr int l96_comp_order(int i) {
-  if constexpr (!IPMC_L96_HALO_FIRST || M < 4) return i;
-  return i == 0 ? 0 : i == 1 ? M - 1 : i == 2 ? M - 2 : i - 2;
-}
-
 template <typename V, int M, int LPC, bool FM, int STAGE, bool IL>
 __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (&acc)[M], V (&ob)[M],
                                           const V (&F)[M], V c, V two, int lane) {
   static_assert(M >= 2, "Lorenz-96 needs at least 2 components per lane");
   const V sr1 = group_next<LPC, IL>(in[0], lane);
-  const V pm2 = group_prev<LPC, IL>(in[M - 2], lane);
-  const V pm1 = group_prev<LPC, IL>(in[M - 1], lane);
-  V cur[M];  // the stage input (values: `in` may alias `xs`)
+  V p2 = group_prev<LPC, IL>(in[M - 2], lane);
+  V p1 = group_prev<LPC, IL>(in[M - 1], lane);
 #pragma unroll
-  for (int j = 0; j < M; ++j) cur[j] = in[j];
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const int j = l96_comp_order<M>(i);
-    const V p2 = j >= 2 ? cur[j - 2] : (j == 1 ? pm1 : pm2);
-    const V p1 = j >= 1 ? cur[j - 1] : pm1;
-    const V xp1 = (j < M - 1) ? cur[j + 1] : sr1;
+  for (int j = 0; j < M; ++j) {
+    const V cur = in[j];
+    const V xp1 = (j < M - 1) ? in[j + 1] : sr1;
     V k;
     if constexpr (FM) {
-      k = madd<true>(xp1 - p2, p1, F[j] - cur[j]);
+      k = madd<true>(xp1 - p2, p1, F[j] - cur);
     } else {
-      V t = -cur[j];
+      V t = -cur;
       t = t - (p1 * p2 - p1 * xp1);
       k = t + F[j];
     }
+    p2 = p1;
+    p1 = cur;
     if constexpr (STAGE == 1) {
       acc[j] = k;
       xs[j] = madd<FM>(c, k, x[j]);
@@ -125,14 +108,6 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
 #pragma unroll
   for (int j = 0; j < M; ++j) asm volatile("" : "+v"(x[j]));
 #endif
-  auto rk4 = [&]() {
-    V acc[M], xs[M];
-    l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);
-    l96_stage<V, M, LPC, FM, 2, IL>(xs, xs, x, acc, ob, F, h2, two, lane);
-    l96_stage<V, M, LPC, FM, 3, IL>(xs, xs, x, acc, ob, F, h, two, lane);
-    l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
-  };
-  int n = 0;
   // R RK4 steps per loop iteration where a lane's step is short (M <= 10):
   // the loop's scalar counter / compare / branch then issue once per R steps.
   // A wave alone on its SIMD (8 192 chains of d=40 on 8 lanes: M = 5, 127
@@ -142,16 +117,34 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
   // one wave per SIMD but not at the headline's two, so M = 20 keeps R = 1
   // (profiles/r6/shard_kernel_ab9.jsonl, shard_kernel_ab10.jsonl).  The
   // loads' s_waitcnt at the loop top, satisfied after the first step, cost
-  // nothing (IPMC_L96_PREWAIT A/B, same files).
+  // nothing (IPMC_L96_PREWAIT A/B, same files).  The R = 1 loop is written
+  // out as before: the packed fp32 headline kernel's VGPR numbering -- worth
+  // 10 % of its time at one wave per SIMD -- follows the source's shape.
   constexpr int R = (M <= IPMC_L96_PAIR_MAX_M) ? IPMC_L96_RK_PER_ITER : 1;
   if constexpr (R > 1) {
+    auto rk4 = [&]() {
+      V acc[M], xs[M];
+      l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);
+      l96_stage<V, M, LPC, FM, 2, IL>(xs, xs, x, acc, ob, F, h2, two, lane);
+      l96_stage<V, M, LPC, FM, 3, IL>(xs, xs, x, acc, ob, F, h, two, lane);
+      l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
+    };
+    int n = 0;
     for (; n + R <= nsteps; n += R) {
 #pragma unroll
       for (int r = 0; r < R; ++r) rk4();
     }
+    for (; n < nsteps; ++n) rk4();
+  } else {
+    IPMC_L96_RK_UNROLL
+    for (int n = 0; n < nsteps; ++n) {
+      V acc[M], xs[M];
+      l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);
+      l96_stage<V, M, LPC, FM, 2, IL>(xs, xs, x, acc, ob, F, h2, two, lane);
+      l96_stage<V, M, LPC, FM, 3, IL>(xs, xs, x, acc, ob, F, h, two, lane);
+      l96_stage<V, M, LPC, FM, 4, IL>(xs, xs, x, acc, ob, F, h6, two, lane);
+    }
   }
-  IPMC_L96_RK_UNROLL
-  for (; n < nsteps; ++n) rk4();
   const V nn = P::of((S)nsteps);
 #pragma unroll
   for (int j = 0; j < M; ++j) g[j] = ob[j] / nn;

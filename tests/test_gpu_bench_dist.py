@@ -93,3 +93,22 @@ def test_bench_cfg5_workload_two_ranks():
     assert line["config"]["total_chains"] == 1 << 20 and line["config"]["chains_per_gpu"] == 1 << 19
     assert line["final_gather"]["mode"] == "mean" and line["final_gather"]["rows"] == 1 << 20
     assert line["value"] > 0
+
+
+def test_bench_one_rank_over_rccl():
+    """`torch.distributed.run --nproc-per-node 1 bench.py` (the driver's launch
+    form with N = 1): the line's barriers, gathers and max over ranks go
+    through a one-rank RCCL group on the MI355X -- the collectives the
+    8-GPU line issues, on hardware (RCCL refuses two ranks on one GPU)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--chains", "8192", "--no-cpu", "--no-extra",
+           "--no-configs", "--no-parity"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and "RCCL" in line["final_gather"]["collective"]
+    assert line["config"]["total_chains"] == 8192 and "8 192 chains" in line["metric"]
+    assert line["value"] > 0 and line["final_gather"]["rows"] == 8192

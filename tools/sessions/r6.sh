@@ -121,6 +121,22 @@ case "$1" in
     # the host trims: the 8 192-chain profile again, then the final session
     bash tools/sessions/r6.sh prof && bash tools/sessions/r6.sh shards && bash tools/sessions/r6.sh final
     ;;
+  s6)
+    # l96_stage back to its round-5 form (the packed fp32 headline's ISA equals
+    # round 5's again): the f32 / f64 headline kernel legs, the 8 192-chain
+    # shard kernel, a kernel trace of the driver's K = 20 line (end-to-end
+    # sweep vs kernel leg), the new one-rank RCCL bench test
+    for i in 1 2; do
+      timeout -k 10 120 python tools/probes/arith_kernel_probe.py s6 40 f32 >> $O/s6_f32.jsonl &&
+      timeout -k 10 120 python tools/probes/arith_kernel_probe.py s6 40 f64 >> $O/s6_f64.jsonl &&
+      timeout -k 10 120 python tools/probes/shard_kernel_probe.py s6 20 8192 2 >> $O/s6_shard.jsonl || exit 1
+    done &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/e2etrace_s6 -o run -- \
+      python bench.py --steps 20 --warmup 5 --no-cpu --no-extra --no-configs --no-parity > $O/e2etrace_s6.json \
+      2> $O/e2etrace_s6.err &&
+    python tools/e2e_trace_summary.py $O/e2etrace_s6 > $O/e2etrace_s6_summary.json &&
+    { tests_ok timeout -k 10 600 $PYT tests/test_gpu_bench_dist.py -k one_rank > $O/pytest_s6.log 2>&1; }
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
