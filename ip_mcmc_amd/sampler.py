@@ -154,6 +154,13 @@ class MCMCSampler:
         # them on the device for the posterior mean); off by default
         self.keep_device_sums = False
         self.last_device_sums = None
+        # pre_sync: a callable f(sums) that a keep="moments" device run calls
+        # with its (sum_u, sum_u2) device tensors after the sweeps are queued
+        # and before its one synchronisation, so that device work on the sums
+        # and its page-locked copies ride the same wait (shard.run_sharded's
+        # block sums); its return value is left in pre_sync_result
+        self.pre_sync = None
+        self.pre_sync_result = None
         # "device" (fused kernels), "host" / "host-generic" (hostloop.py) for the last run
         self.last_path = None
         self.last_run_timing = None
@@ -186,7 +193,7 @@ class MCMCSampler:
             raise ValueError("results='device' keeps keep='moments' or 'last' in HBM")
         on_dev = results == "device"
         t_entry = time.perf_counter()
-        self.last_device_sums = None
+        self.last_device_sums = self.pre_sync_result = None
         try:
             plan = _Plan(self.proposer, self.accepter)
         except UnsupportedOnDevice as e:
@@ -458,7 +465,9 @@ class MCMCSampler:
         state_host = [None if on_dev else _pinned_copy(U)] + [_pinned_copy(t) for t in (phi, accepts, calls)
                                                               if t is not None]
         sums_host = None if (sums is None or on_dev) else [_pinned_copy(t) for t in sums]
+        pre = self.pre_sync(sums) if (self.pre_sync is not None and sums is not None) else None
         torch.cuda.synchronize(device)
+        self.pre_sync_result = pre
         self.last_run_seconds = time.perf_counter() - t0
 
         total = step - rng.step

@@ -106,7 +106,36 @@ def _split(lo, hi, block):
     return head, (fb, lb), tail
 
 
-def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
+def _rank_parts(rows, lo, block, div=1.0):
+    """A rank's contribution to the posterior mean's block sums, for its rows
+    [lo, lo + n) of the global chain order: (F, shared) -- F the sums of its
+    whole blocks (device rows: ipmc_block_sums, queued on the current stream),
+    shared the rows of the at most two blocks it shares with other ranks."""
+    n, k = int(rows.shape[0]), int(rows.shape[1])
+    head, (b0, b1), tail = _split(lo, lo + n, block)
+    on_dev = isinstance(rows, torch.Tensor) and rows.is_cuda
+    if b1 > b0:
+        f0, f1 = b0 * block - lo, b1 * block - lo
+        if on_dev:
+            from . import device as D
+
+            F = D.block_sums(rows[f0:f1], block, div)
+        else:
+            F = _host_block_sums(rows[f0:f1], div, block)
+    else:
+        F = torch.zeros((0, k), dtype=torch.float64, device=rows.device) if on_dev else np.zeros((0, k))
+    return F, [rows[seg[0] - lo : seg[1] - lo] for seg in (head, tail) if seg is not None]
+
+
+def _to_host_async(t):
+    """A device tensor's page-locked host copy, queued on the current stream
+    (valid once the stream is synchronised)."""
+    h = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    return h
+
+
+def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK, parts=None):
     """block_sum over the chains of all ranks in global (rank) order, each rank
     holding its own rows: a rank sums its whole blocks (on the device when
     `local` is a CUDA tensor: ipmc_block_sums, one launch) and contributes those
@@ -116,7 +145,9 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
     order).  Bit-identical to block_sum over the gathered rows, without
     gathering them (config 5's per-chain sums are 4 GB), and no rank waits on
     another's sum: one all_gather of ~k / block of the data instead of P - 1
-    sequential hops."""
+    sequential hops.  parts: this rank's (F, shared) already formed and on
+    the host (_rank_parts at the rank's global offset; run_sharded queues them
+    before the run's synchronisation)."""
     rank, world = world_info(group)
     on_dev = isinstance(local, torch.Tensor) and local.is_cuda
     shape = tuple(local.shape[1:])
@@ -137,19 +168,12 @@ def ordered_sum_sharded(local, group=None, div=1.0, block=MEAN_BLOCK):
         counts = [n_local]
     los = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     lo = int(los[rank])
-    head, (b0, b1), tail = _split(lo, lo + n_local, block)
-    if b1 > b0:  # this rank's whole blocks, in one call
-        f0, f1 = b0 * block - lo, b1 * block - lo
-        if on_dev:
-            from . import device as D
-
-            F = D.block_sums(rows[f0:f1], block, div).cpu().numpy()
-        else:
-            F = _host_block_sums(rows[f0:f1], div, block)
+    if parts is None:  # this rank's whole blocks in one call, its shared rows
+        F, shared = _rank_parts(rows, lo, block, div)
+        F = F.cpu().numpy() if on_dev else F
+        shared = [p.cpu().numpy() if on_dev else p for p in shared]
     else:
-        F = np.zeros((0, k))
-    shared = [rows[seg[0] - lo : seg[1] - lo] for seg in (head, tail) if seg is not None]
-    shared = [p.cpu().numpy() if on_dev else p for p in shared]
+        F, shared = parts
     mine = np.concatenate([F.reshape(-1)] + [p.reshape(-1) for p in shared]) if (len(F) or shared) else np.zeros(0)
 
     def size(r):  # every rank's contribution, known from the counts alone
@@ -293,8 +317,16 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
     if sampler.chain_offset != lo:
         raise ValueError(f"make_sampler must build the sampler with chain_offset={lo}, got {sampler.chain_offset}")
     # gather="mean": the posterior mean's block sums run on the device sums the
-    # sweeps left (MCMCSampler.last_device_sums) when the run was a device run
+    # sweeps left (MCMCSampler.last_device_sums) when the run was a device run,
+    # queued before the run's one synchronisation (pre_sync), their host copies
+    # page-locked
     sampler.keep_device_sums = gather == "mean"
+    if gather == "mean":
+        def _queue_block_sums(sums):
+            F, shared = _rank_parts(sums[0], lo, MEAN_BLOCK)
+            return [_to_host_async(F)] + [_to_host_async(p) for p in shared]
+
+        sampler.pre_sync = _queue_block_sums
     if not isinstance(local_u0, torch.Tensor):
         local_u0 = np.asarray(local_u0, dtype=np.float64)
     sf = None if sample_file is None else f"{sample_file}.rank{rank}.npy"
@@ -320,8 +352,10 @@ def run_sharded(make_sampler, u_0, n_samples, burn_in=1000, sample_interval=200,
         n = max(1, res["n"])
         dsum = getattr(sampler, "last_device_sums", None)
         rows = dsum[0] if dsum is not None else res["sum_u"].reshape(hi - lo, k)
-        mean = ordered_sum_sharded(rows, group) / (float(n) * n_total)
-        sampler.last_device_sums = None
+        pre = sampler.pre_sync_result if dsum is not None else None
+        parts = None if pre is None else (pre[0].numpy(), [p.numpy() for p in pre[1:]])
+        mean = ordered_sum_sharded(rows, group, parts=parts) / (float(n) * n_total)
+        sampler.last_device_sums = sampler.pre_sync = sampler.pre_sync_result = None
         # a device state is the checkpoint's own tensor (in the run's dtype):
         # hand out an f64 copy, as the host path and MCMCSampler.run(keep='last') do
         u_out = cols[0].to(torch.float64, copy=True) if isinstance(cols[0], torch.Tensor) else cols[0]
