@@ -137,6 +137,15 @@ case "$1" in
     python tools/e2e_trace_summary.py $O/e2etrace_s6 > $O/e2etrace_s6_summary.json &&
     { tests_ok timeout -k 10 600 $PYT tests/test_gpu_bench_dist.py -k one_rank > $O/pytest_s6.log 2>&1; }
     ;;
+  s7)
+    # block sums queued before run()'s one synchronisation (pre_sync): the
+    # sharding / sampler tests, the 8 192-chain end-to-end profile, the shares
+    tests_ok timeout -k 10 900 $PYT tests/test_gpu_shard.py tests/test_gpu_run.py tests/test_gpu_sampler_edges.py \
+      tests/test_gpu_bench_dist.py > $O/pytest_s7.log 2>&1
+    timeout -k 10 200 python tools/probes/shard_e2e_profile.py 8192 20 4 s7 >> $O/shard_e2e_s7.jsonl \
+      2> $O/shard_e2e_prof_s7.txt &&
+    SHARDS_TAG=_s7 bash tools/sessions/r6.sh shards
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
@@ -181,7 +190,7 @@ case "$1" in
     for i in 1 2; do
       for c in 32768 16384 8192; do
         timeout -k 10 300 python bench.py --chains $c --steps 20 --warmup 5 --no-cpu --no-extra --no-configs \
-          --no-parity >> $O/shards_k20.jsonl 2>> $O/shards.err || exit 1
+          --no-parity >> $O/shards_k20${SHARDS_TAG:-}.jsonl 2>> $O/shards.err || exit 1
       done
     done
     ;;
