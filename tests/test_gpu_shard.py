@@ -283,3 +283,40 @@ def test_rccl_collectives_of_the_product_path(tmp_path):
                       ("acc_m", one["accepts"])):
         assert np.array_equal(got[key], want), key
     assert float(got["mx"]) == 2.5
+
+
+def _mean_worker_n(rank, world, port, out_path, n_total):
+    sys.path.insert(0, REPO)
+    from ip_mcmc_amd.shard import chain_range, run_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = chain_range(n_total, rank, world)
+    u0 = torch.as_tensor(0.1 * np.random.default_rng(9).normal(size=(n_total, K))[lo:hi], device="cuda:0")
+    res = run_sharded(_make_sampler, u0, n_samples=1, burn_in=0, sample_interval=4, keep="moments", gather="mean",
+                      results="device", n_total=n_total)
+    assert res["sampler"].pre_sync_result is None  # consumed
+    if rank == 1:
+        np.savez(out_path, mean=res["mean"], phi=res["phi"], acc=res["accepts"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_run_sharded_mean_with_whole_and_shared_blocks_two_ranks(tmp_path):
+    """5 003 chains over two ranks (gloo, both on cuda:0), rank-local u_0 on the
+    device: each rank's whole blocks of 1 024 chains summed on the device and
+    its shared rows copied to the host before the run's one synchronisation
+    (MCMCSampler.pre_sync) -- the mean, Φ and accept counts equal one
+    process's bit for bit."""
+    from ip_mcmc_amd.shard import block_sum, run_sharded
+
+    n_total = 5003
+    u0 = 0.1 * np.random.default_rng(9).normal(size=(n_total, K))
+    one = run_sharded(_make_sampler, u0, n_samples=1, burn_in=0, sample_interval=4, keep="moments", gather="all")
+    assert np.array_equal(one["mean"], block_sum(one["sum_u"]) / (4.0 * n_total))
+    out = str(tmp_path / "m2.npz")
+    mp.start_processes(_mean_worker_n, args=(2, _free_port(), out, n_total), nprocs=2, start_method="spawn")
+    got = np.load(out)
+    assert np.array_equal(got["mean"], one["mean"])
+    assert np.array_equal(got["phi"], one["phi"]) and np.array_equal(got["acc"], one["accepts"])
