@@ -62,17 +62,6 @@ __device__ __forceinline__ void l96_stage(V (&in)[M], V (&xs)[M], V (&x)[M], V (
   }
 }
 
-// experiments: RK4 steps per loop iteration (-DIPMC_L96_UNROLL=2); default: the compiler's choice
-#if defined(IPMC_L96_UNROLL) && IPMC_L96_UNROLL > 0
-#define IPMC_L96_STR_(x) #x
-#define IPMC_L96_UNROLL_PRAGMA(n) _Pragma(IPMC_L96_STR_(unroll n))
-#define IPMC_L96_RK_UNROLL IPMC_L96_UNROLL_PRAGMA(IPMC_L96_UNROLL)
-#else
-#define IPMC_L96_RK_UNROLL
-#endif
-#ifndef IPMC_L96_PREWAIT  // experiments: 0 = the loads of x(0) waited for inside the RK loop
-#define IPMC_L96_PREWAIT 0
-#endif
 // IPMC_L96_RK_PER_ITER RK4 steps per loop iteration up to IPMC_L96_PAIR_MAX_M
 // components per lane (l96_forward; profiles/r6/shard_kernel_ab10.jsonl)
 #ifndef IPMC_L96_PAIR_MAX_M
@@ -99,15 +88,6 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     x[j] = P::of(x0[j]);
     ob[j] = P::of((S)0);
   }
-#if IPMC_L96_PREWAIT
-  // x(0) is first read inside the RK loop, so the memory-wait pass put its
-  // s_waitcnt at the loop top, where it issues every RK4 step (2 of the 129
-  // instructions per step at 8 lanes per chain, whose one wave per SIMD
-  // issues every instruction in its own 4-cycle slot).  An opaque use here
-  // makes the loads complete before the loop.
-#pragma unroll
-  for (int j = 0; j < M; ++j) asm volatile("" : "+v"(x[j]));
-#endif
   // R RK4 steps per loop iteration where a lane's step is short (M <= 10):
   // the loop's scalar counter / compare / branch then issue once per R steps.
   // A wave alone on its SIMD (8 192 chains of d=40 on 8 lanes: M = 5, 127
@@ -117,7 +97,7 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
   // one wave per SIMD but not at the headline's two, so M = 20 keeps R = 1
   // (profiles/r6/shard_kernel_ab9.jsonl, shard_kernel_ab10.jsonl).  The
   // loads' s_waitcnt at the loop top, satisfied after the first step, cost
-  // nothing (IPMC_L96_PREWAIT A/B, same files).  The R = 1 loop is written
+  // nothing (the `pw` A/B, same files).  The R = 1 loop is written
   // out as before: the packed fp32 headline kernel's VGPR numbering -- worth
   // 10 % of its time at one wave per SIMD -- follows the source's shape.
   constexpr int R = (M <= IPMC_L96_PAIR_MAX_M) ? IPMC_L96_RK_PER_ITER : 1;
@@ -136,7 +116,6 @@ __device__ __forceinline__ void l96_forward(const V (&F)[M], const S* __restrict
     }
     for (; n < nsteps; ++n) rk4();
   } else {
-    IPMC_L96_RK_UNROLL
     for (int n = 0; n < nsteps; ++n) {
       V acc[M], xs[M];
       l96_stage<V, M, LPC, FM, 1, IL>(x, xs, x, acc, ob, F, h2, two, lane);
