@@ -244,6 +244,30 @@ def test_sweep_l96_interleaved_8_lanes_box_rw_schedule(dev, orc, dtype, cpl, K):
         _assert_same(d, o, (K, str(dtype), cpl, sorted(kw)))
 
 
+@pytest.mark.parametrize("dtype,cpl", [(torch.float64, 1), (torch.float32, 2)])
+@pytest.mark.parametrize("lanes", [4, 8])
+def test_sweep_l96_rk_steps_not_a_multiple_of_the_unroll(dev, orc, dtype, cpl, lanes):
+    """Up to 10 components per lane the RK4 loop runs 4 steps per iteration
+    and the remaining 1-3 after it (l96_forward, round 6): forward maps of 1,
+    2, 3, 5, 7 and 41 RK4 steps (d=40 on 4 and 8 lanes: 10 and 5 components),
+    both arithmetics, sweeps with sums -- the oracle's bits."""
+    from ip_mcmc_amd import Lorenz96Operator
+
+    for n_rk in (1, 2, 3, 5, 7, 41):
+        for arith in ("fma", "reference"):
+            op = Lorenz96Operator(40, 8.0, dt=0.005, n_steps=n_rk, arith=arith)
+            U0, phi0, y, ginv, sq = _problem(op, 131, dtype, orc, seed=n_rk)
+            d = _sweep_device(op, U0, phi0, y, ginv, sq, 0.25, 31, 2, 5, dtype, dev, lanes=lanes, cpl=cpl,
+                              want_sums=True)
+            o = _sweep_oracle(orc, op, U0, phi0, y, ginv, sq, 0.25, 31, 2, 5, dtype, want_sums=True)
+            _assert_same(d, o, (n_rk, arith, lanes, str(dtype)))
+            assert np.array_equal(d["sum_u"], o["sum_u"]) and np.array_equal(d["sum_u2"], o["sum_u2"])
+            # G and Φ alone (the eval kernels, auto layout for 16 384 chains: 4 lanes, 10 components)
+            U = 0.3 * np.random.default_rng(n_rk).normal(size=(16384, 40))
+            g = op.forward_device(_t(U, dtype, dev)).cpu().numpy()
+            assert np.array_equal(g, orc.forward(op, U, _np(dtype))), (n_rk, arith)
+
+
 def test_sweep_l96_d256_subset_bit_exact(dev, orc):
     """Config 5 shape at reduced length (d=256, 500 RK4 steps, 4096 chains), auto layouts."""
     from ip_mcmc_amd import Lorenz96Operator
