@@ -146,6 +146,11 @@ case "$1" in
       2> $O/shard_e2e_prof_s7.txt &&
     SHARDS_TAG=_s7 bash tools/sessions/r6.sh shards
     ;;
+  s8)
+    # RK4 step counts that are not a multiple of the 4-step unroll
+    tests_ok timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "multiple_of_the_unroll or interleaved_8 or forward_and_potential" \
+      > $O/pytest_s8.log 2>&1
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
