@@ -151,6 +151,18 @@ case "$1" in
     tests_ok timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "multiple_of_the_unroll or interleaved_8 or forward_and_potential" \
       > $O/pytest_s8.log 2>&1
     ;;
+  ab12)
+    # the packed fp32 headline kernel: product vs the mid-round source (the RK4
+    # step as a lambda in a counted loop, 6a006ca: other VGPR numbering) vs the
+    # l96_stage rewrite alone (stagecopy: the product's RK loop byte for byte),
+    # interleaved three times
+    for i in 1 2 3; do
+      for v in product r6mid stagecopy; do
+        L=""; [ $v != product ] && L=ip_mcmc_amd/lib/variants/$v/libipmc.so
+        IPMC_LIB_PATH=$L timeout -k 10 120 python tools/probes/arith_kernel_probe.py $v 40 f32 >> $O/ab12_f32.jsonl || exit 1
+      done
+    done
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
