@@ -71,8 +71,8 @@ def test_headline_kernel_register_count_is_the_measured_one(kernels):
 # The RK4 loops of the measured kernels, as the library holds them (llvm-objdump
 # of the code objects): instruction mix per loop iteration and a fingerprint of
 # the instruction text with its register numbering.  The packed fp32 headline
-# runs one wave per SIMD, where its VGPR numbering alone moved it 1.71 -> 1.96 ms
-# (round 6: a source rewrite with identical instructions); the fp64
+# runs one wave per SIMD, where its VGPR numbering alone moved it 1.68 -> 1.86 ms
+# (round 6: the RK4 step written as a lambda, identical instructions); the fp64
 # headline's schedule is the one the roofline numbers were measured on.  A
 # change here is not an error by itself: re-measure the kernel
 # (tools/probes/arith_kernel_probe.py, shard_kernel_probe.py) and record the
