@@ -562,8 +562,9 @@ def main():
     ap.add_argument("--chains", type=int, default=None,
                     help="total chains (strong, the default) or chains per GPU (weak); default: the workload's")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
-                    help="weak: --chains per GPU (cfg3's default: 65 536 chains on every GPU); strong: --chains "
-                         "split over the GPUs (cfg4 / cfg5's default: their ensembles are stated per node)")
+                    help="strong (the default for every workload: BASELINE states the ensembles per node, cfg3's "
+                         "metric 65 536 chains over the whole node): --chains split over the GPUs; weak: --chains on "
+                         "every GPU")
     ap.add_argument("--steps-per-launch", type=int, default=0,
                     help="pCN steps per kernel launch of the kernel leg (0 = auto)")
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
