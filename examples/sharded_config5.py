@@ -41,7 +41,9 @@ def main():
     y = G(0.5 * np.sin(2 * np.pi * k / D)) + 0.1 * np.random.default_rng(3).normal(size=D)
     noise = GaussianDistribution(np.zeros(D), 0.01 * np.eye(D))
     prior = GaussianDistribution(np.zeros(D), np.eye(D))
-    u0 = np.full((chains, D), 0.0)
+    # this rank's own rows of the node's u_0 only (run_sharded(n_total=)): no
+    # rank allocates the 2^20 x 256 ensemble
+    u0 = lambda lo, hi: np.zeros((hi - lo, D))  # noqa: E731
     means = {}
     for dtype in (np.float64, np.float32):
         def make(chain_offset=0):
@@ -51,7 +53,8 @@ def main():
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        res = run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=steps, keep="moments", gather="mean")
+        res = run_sharded(make, u0, n_samples=1, burn_in=0, sample_interval=steps, keep="moments", gather="mean",
+                          n_total=chains)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
