@@ -163,6 +163,10 @@ case "$1" in
       done
     done
     ;;
+  s9)
+    # the examples (config 5 with a rank-local u_0) and the sharding tests on the final tree
+    tests_ok timeout -k 10 900 $PYT tests/test_gpu_examples.py tests/test_gpu_shard.py > $O/pytest_s9.log 2>&1
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
