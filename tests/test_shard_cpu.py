@@ -171,7 +171,18 @@ def _osum_worker(rank, world, port, out_path, n_total, block, div):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = chain_range(n_total, rank, world)
-    got = ordered_sum_sharded(_osum_rows(n_total)[lo:hi], div=div, block=block)
+    rows = _osum_rows(n_total)[lo:hi]
+    got = ordered_sum_sharded(rows, div=div, block=block)
+    # the rank's whole-block sums and shared rows formed ahead (run_sharded's
+    # pre_sync path, here on host rows): the same bits
+    from ip_mcmc_amd.shard import _rank_parts
+
+    assert np.array_equal(ordered_sum_sharded(rows, div=div, block=block, parts=_rank_parts(rows, lo, block, div)),
+                          got)
+    # bench.py's max over ranks of the wall time (gloo: on the host)
+    import bench
+
+    assert bench.max_over_ranks(float(rank), world, "cpu") == float(world - 1)
     if rank == world - 1:
         np.save(out_path, got)
     dist.barrier()
