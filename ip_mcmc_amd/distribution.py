@@ -64,7 +64,8 @@ class GaussianDistribution(DistributionBase):
 
     def centred(self):
         """N(0, C) sharing this distribution's covariance and its factor L (no
-        second factorization)."""
+        second factorization, and its diagonal test decided once for both)."""
+        self.is_diagonal  # noqa: B018 -- cached on self, so the copy carries it
         w = object.__new__(type(self))
         w.__dict__.update(self.__dict__)
         w.mean = np.zeros_like(self.mean)
