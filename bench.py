@@ -481,7 +481,10 @@ def config_line(key, dev, world, steps=None, warmup=None, chains=None):
                     "part the paired streams at the first steps (fma_paired_identical_accept_frac); their claim is "
                     "the stated stationary tolerance.  REFERENCE arith issues 32 FP64 ops (no FMA) per component "
                     "and RK4 step plus 24 DPP moves per 16 components (the d=256 kernel's loop, hipcc -S): "
-                    "30 FLOP / (2 x 33.5 slots) = 0.448 of the FP64 peak is its op-mix ceiling"}
+                    "30 FLOP / (2 x 33.5 slots) = 0.448 of the FP64 peak is its op-mix ceiling (at the ~2.15 GHz "
+                    "the chip holds under this load, ~0.40).  reference_frac_of_peak is end to end over the "
+                    "run's steps + Phi(u_0), which counts no FLOP of Phi(u_0): with 4 steps the kernel's own "
+                    "fraction is 5/4 of it"}
     return out
 
 
