@@ -167,6 +167,11 @@ case "$1" in
     # the examples (config 5 with a rank-local u_0) and the sharding tests on the final tree
     tests_ok timeout -k 10 900 $PYT tests/test_gpu_examples.py tests/test_gpu_shard.py > $O/pytest_s9.log 2>&1
     ;;
+  suite)
+    # the whole GPU suite and smoke on the tree as it stands
+    tests_ok timeout -k 10 1200 $PYT tests -m gpu > $O/pytest_gpu_suite.log 2>&1
+    timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_suite.txt 2>&1
+    ;;
   gloo8)
     # the driver's 8-GPU line rehearsed with gloo, all eight ranks on the one
     # GPU (strong scaling by default: 65 536 chains over the node under
